@@ -1,0 +1,148 @@
+"""ORACLE (test infrastructure only) — greedy Whisper decoding with the logits
+processors faster-whisper asks CTranslate2 to apply (upstream, not vendored).
+
+Options mirror faster-whisper 1.2.1's ``transcribe`` defaults as called by the
+reference (``src/backends/faster_whisper.py:235-245``) with ``beam_size=1`` for the
+greedy parity mode: ``suppress_blank=True``, ``suppress_tokens=[-1]`` (expanded by
+``get_suppressed_tokens``), ``without_timestamps=False``,
+``max_initial_timestamp=1.0`` (index 50), ``max_length=448`` positions.
+
+The processors follow openai-whisper's ``SuppressBlank``, ``SuppressTokens`` and
+``ApplyTimestampRules`` (in-container restatement: transformers
+``generation/logits_process.py:1816,1869,1909``).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+NEG_INF = -np.inf
+
+
+def log_softmax(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.float64)
+    m = np.max(x)
+    return x - (m + np.log(np.sum(np.exp(x - m))))
+
+
+def logsumexp(x: np.ndarray) -> float:
+    x = x.astype(np.float64)
+    m = np.max(x)
+    if not np.isfinite(m):
+        return float(m)
+    return float(m + np.log(np.sum(np.exp(x - m))))
+
+
+@dataclass
+class DecodeOptions:
+    suppress_blank: bool = True
+    suppress_tokens: tuple = ()
+    without_timestamps: bool = False
+    max_initial_timestamp_index: int = 50
+    max_length: int = 448
+
+
+def process_logits(logits: np.ndarray, sampled: list, st, opts: DecodeOptions) -> np.ndarray:
+    """Apply the logits filters for the next token given the tokens sampled so far."""
+    x = logits.astype(np.float64).copy()
+    n = len(sampled)
+    tb = st.timestamp_begin
+    if opts.suppress_blank and n == 0:
+        x[[st.blank, st.eot]] = NEG_INF
+    if len(opts.suppress_tokens):
+        x[list(opts.suppress_tokens)] = NEG_INF
+    if not opts.without_timestamps:
+        x[st.no_timestamps] = NEG_INF
+        last = n >= 1 and sampled[-1] >= tb
+        pen = n < 2 or sampled[-2] >= tb
+        if last:
+            if pen:
+                x[tb:] = NEG_INF
+            else:
+                x[:st.eot] = NEG_INF
+        ts = [t for t in sampled if t >= tb]
+        if ts:
+            tl = ts[-1] if (last and not pen) else ts[-1] + 1
+            x[tb:tl] = NEG_INF
+        if n == 0:
+            x[:tb] = NEG_INF
+            if opts.max_initial_timestamp_index is not None:
+                x[tb + opts.max_initial_timestamp_index + 1:] = NEG_INF
+        lp = log_softmax(x)
+        if logsumexp(lp[tb:]) > np.max(lp[:tb]):
+            x[:tb] = NEG_INF
+    return x
+
+
+@dataclass
+class WindowResult:
+    tokens: list
+    sum_logprob: float
+    no_speech_prob: float
+    language: int
+    step_logits: list = field(default_factory=list)   # raw fp32 logits per generated step
+    prompt_logits: list = field(default_factory=list)
+
+
+def detect_language(raw_sot_logits: np.ndarray, st) -> int:
+    lang = raw_sot_logits[st.first_lang:st.first_lang + st.n_langs]
+    return st.first_lang + int(np.argmax(lang))
+
+
+def no_speech_prob(raw_sot_logits: np.ndarray, st) -> float:
+    return float(np.exp(log_softmax(raw_sot_logits)[st.no_speech]))
+
+
+def greedy_window(oracle, mel_window, st, *, language=None, task=None, prev_tokens=(),
+                  opts: DecodeOptions = DecodeOptions(), keep_logits: int = 0) -> WindowResult:
+    """Encode one 30 s window and decode greedily (faster-whisper get_prompt + CT2 generate)."""
+    enc = oracle.encode(mel_window)
+    xkv = oracle.cross_kv(enc)
+    return greedy_from_encoder(oracle, xkv, st, language=language, task=task, prev_tokens=prev_tokens,
+                               opts=opts, keep_logits=keep_logits)
+
+
+def greedy_from_encoder(oracle, xkv, st, *, language=None, task=None, prev_tokens=(),
+                        opts: DecodeOptions = DecodeOptions(), keep_logits: int = 0) -> WindowResult:
+    task = st.transcribe if task is None else task
+    cache = oracle.new_cache()
+    prompt = []
+    if prev_tokens:
+        prompt.append(st.sot_prev)
+        prompt.extend(list(prev_tokens)[-(opts.max_length // 2 - 1):])
+    sot_index = len(prompt)
+    prompt.append(st.sot)
+    pos = 0
+    prompt_logits = []
+    for t in prompt:                      # feed up to and including SOT
+        lg = oracle.decoder_step(t, pos, cache, xkv)
+        pos += 1
+    raw_sot = lg
+    prompt_logits.append(raw_sot)
+    lang = detect_language(raw_sot, st) if language is None else language
+    nsp = no_speech_prob(raw_sot, st)
+    rest = [lang, task] + ([st.no_timestamps] if opts.without_timestamps else [])
+    for t in rest:
+        lg = oracle.decoder_step(t, pos, cache, xkv)
+        pos += 1
+    prompt_len = len(prompt) + len(rest)
+    sampled: list = []
+    sum_lp = 0.0
+    step_logits = []
+    while True:
+        if keep_logits and len(step_logits) < keep_logits:
+            step_logits.append(lg.copy())
+        x = process_logits(lg, sampled, st, opts)
+        nxt = int(np.argmax(x))
+        sum_lp += float(log_softmax(x)[nxt])
+        if nxt == st.eot:
+            break
+        sampled.append(nxt)
+        if prompt_len + len(sampled) >= opts.max_length:
+            break
+        lg = oracle.decoder_step(nxt, pos, cache, xkv)
+        pos += 1
+    del sot_index
+    return WindowResult(tokens=sampled, sum_logprob=sum_lp, no_speech_prob=nsp, language=lang,
+                        step_logits=step_logits, prompt_logits=prompt_logits)

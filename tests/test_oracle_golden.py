@@ -1,0 +1,115 @@
+"""The oracle (CPU restatement) pinned against the committed golden vectors
+(tools/make_golden.py; transformers 5.15.0 as the independent implementation)."""
+import os
+
+import numpy as np
+import pytest
+
+from open_speech_amd import dims as D
+from open_speech_amd import synth, weights
+from open_speech_amd.tokenizer import WhisperTokenizer, get_suppressed_tokens
+from oracle import decode as odec
+from oracle import mel as omel
+from oracle.model import WhisperOracle
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.mark.parametrize("name", ["chirp30", "tone7", "silence5", "chirp3"])
+def test_mel_matches_golden(name):
+    z = np.load(os.path.join(GOLD, f"mel_{name}.npz"))
+    x = omel.pcm16_to_float(z["pcm"])
+    mel = omel.log_mel(x, int(z["n_mels"]))
+    assert mel.shape == z["mel"].shape
+    np.testing.assert_allclose(mel, z["mel"], atol=2e-5, rtol=0)
+
+
+def test_mel_frame_count():
+    assert omel.n_frames_for(480000) == 3001
+    assert omel.n_frames_for(0) == 1
+
+
+def test_mel_filters_shape_and_norm():
+    f = omel.mel_filters(128)
+    assert f.shape == (128, 201)
+    assert (f >= 0).all()
+    # every filter has support, slaney area normalisation
+    assert (f.sum(1) > 0).all()
+
+
+def test_logits_rules_match_golden():
+    z = np.load(os.path.join(GOLD, "logits_rules.npz"))
+    st = D.SpecialTokens.for_vocab(51866)
+    tok = WhisperTokenizer(51866)
+    sup = get_suppressed_tokens(tok, [-1])
+    assert tuple(z["suppress"].tolist()) == sup
+    opts = odec.DecodeOptions(suppress_tokens=sup)
+    off = 0
+    for i, n in enumerate(z["hist_len"]):
+        hist = z["hist"][off:off + n].tolist()
+        off += n
+        ci, variant = divmod(i, 2)
+        rng = np.random.default_rng(100 + 2 * ci + variant)
+        lg = rng.standard_normal(51866).astype(np.float32) * 2.0
+        if variant == 1:
+            lg[st.timestamp_begin:] += 4.0
+        x = odec.process_logits(lg, hist, st, opts)
+        mask = np.packbits(~np.isfinite(x))
+        assert np.array_equal(mask, z["masks"][i]), f"case {i} hist={hist}"
+        assert int(np.argmax(x)) == int(z["argmax"][i])
+
+
+@pytest.fixture(scope="module")
+def tiny():
+    d = D.TINY_TEST
+    w = weights.random_weights(d, seed=1234, emb_std=0.5)
+    return d, w, np.load(os.path.join(GOLD, "tiny_model.npz"))
+
+
+def test_tiny_encoder_fp32_matches_transformers(tiny):
+    d, w, z = tiny
+    enc = WhisperOracle(d, w, fp16=False).encode(z["mel"])
+    np.testing.assert_allclose(enc, z["enc"].astype(np.float32), atol=4e-3, rtol=0)
+
+
+def test_tiny_greedy_fp32_matches_transformers(tiny):
+    d, w, z = tiny
+    st = D.SpecialTokens.for_vocab(d.n_vocab)
+    orc = WhisperOracle(d, w, fp16=False)
+    sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+    opts = odec.DecodeOptions(suppress_tokens=sup)
+    enc = orc.encode(z["mel"])
+    r = odec.greedy_from_encoder(orc, orc.cross_kv(enc), st, opts=opts, keep_logits=8)
+    assert r.language == int(z["language"])
+    assert abs(r.no_speech_prob - float(z["no_speech_prob"])) < 1e-4
+    np.testing.assert_allclose(r.prompt_logits[0], z["sot_logits"], atol=2e-3, rtol=0)
+    for i in range(8):
+        np.testing.assert_allclose(r.step_logits[i], z["step_logits"][i], atol=2e-3, rtol=0)
+    assert r.tokens == z["ids"].tolist()
+    assert abs(r.sum_logprob - float(z["sum_logprob"])) < 1e-2 * max(1.0, abs(float(z["sum_logprob"])))
+
+
+@pytest.mark.slow
+def test_turbo_encoder_layer_fp32_matches_transformers():
+    z = np.load(os.path.join(GOLD, "turbo_enc_layer0.npz"))
+    d = D.LARGE_V3_TURBO
+    specs = weights.canonical_specs(d)
+    idx = {s.name: i for i, s in enumerate(specs)}
+    w = {}
+    for s in specs:
+        if s.name.startswith("enc.l0."):
+            w[s.name] = weights.make_tensor(s, d, int(z["w_seed"]), idx[s.name])
+    x = weights.hash_uniform(int(z["x_seed"]), 0, 1500 * 1280, 1.0, 0.0).reshape(1500, 1280)
+    import dataclasses
+    d1 = dataclasses.replace(d, n_audio_layer=1)
+    orc = WhisperOracle(d1, w, fp16=False)
+    y = orc.encoder_layer(0, x)
+    np.testing.assert_allclose(y[z["rows"]], z["y_rows"], atol=2e-4, rtol=0)
+    np.testing.assert_allclose(np.linalg.norm(y.astype(np.float64), axis=1), z["y_rownorm"], rtol=1e-5)
+
+
+def test_synth_clip_levels():
+    pcm = synth.chirp_clip(0, 30.0)
+    assert pcm.dtype == np.int16 and len(pcm) == 480000
+    rms = np.sqrt(np.mean((pcm / 32768.0) ** 2))
+    assert abs(20 * np.log10(rms) + 18.0) < 0.5

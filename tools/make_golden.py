@@ -1,0 +1,252 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/ (run here, on CPU; committed).
+
+The reference (faster-whisper 1.2.1 + CTranslate2) is not installed and cannot be
+fetched, and the reference's own tests pin no numbers for this path.
+The fixtures therefore come from an independent implementation of the same
+published algorithm that IS in the image: transformers 5.15.0
+(``WhisperFeatureExtractor``, ``WhisperForConditionalGeneration`` in fp32, and its
+Whisper logits processors), with random weights from the canonical hash init so
+that tests can regenerate the weights instead of storing them.
+
+Usage:  python tools/make_golden.py [--out tests/golden]
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import osw_path  # noqa: E402
+
+osw_path.load()
+from open_speech_amd import dims as D  # noqa: E402
+from open_speech_amd import synth, weights  # noqa: E402
+from open_speech_amd.tokenizer import WhisperTokenizer, get_suppressed_tokens  # noqa: E402
+
+from transformers import GenerationConfig, WhisperConfig, WhisperFeatureExtractor  # noqa: E402
+from transformers import WhisperForConditionalGeneration  # noqa: E402
+from transformers.generation.logits_process import (  # noqa: E402
+    SuppressTokensAtBeginLogitsProcessor, SuppressTokensLogitsProcessor,
+    WhisperTimeStampLogitsProcessor)
+
+TINY_SEED = 1234
+TINY_EMB_STD = 0.5
+TURBO_LAYER_SEED = 77
+
+
+def hf_config(d: D.WhisperDims) -> WhisperConfig:
+    return WhisperConfig(vocab_size=d.n_vocab, num_mel_bins=d.n_mels, encoder_layers=d.n_audio_layer,
+                         encoder_attention_heads=d.n_audio_head, decoder_layers=d.n_text_layer,
+                         decoder_attention_heads=d.n_text_head, d_model=d.n_audio_state,
+                         encoder_ffn_dim=4 * d.n_audio_state, decoder_ffn_dim=4 * d.n_text_state,
+                         max_source_positions=d.n_audio_ctx, max_target_positions=d.n_text_ctx,
+                         pad_token_id=50257, bos_token_id=50257, eos_token_id=50257,
+                         decoder_start_token_id=50258, attn_implementation="eager")
+
+
+def fe_mel(pcm: np.ndarray, n_mels: int) -> np.ndarray:
+    """transformers' extractor applied to faster-whisper's 160-sample-padded waveform."""
+    fe = WhisperFeatureExtractor(feature_size=n_mels)
+    x = pcm.astype(np.float32) / 32768.0
+    x = np.pad(x, (0, 160))
+    return fe._np_extract_fbank_features(x[None, :], "cpu")[0].astype(np.float32)
+
+
+def gen_mel(out):
+    clips = {
+        "chirp30": (synth.chirp_clip(0, 30.0), 128),
+        "tone7": (synth.tone_clip(7.3), 80),
+        "silence5": (synth.silence_clip(5.0), 128),
+        "chirp3": (synth.chirp_clip(5, 3.21), 80),
+    }
+    meta = {}
+    for name, (pcm, n_mels) in clips.items():
+        mel = fe_mel(pcm, n_mels)
+        np.savez_compressed(os.path.join(out, f"mel_{name}.npz"), pcm=pcm, mel=mel,
+                            n_mels=np.int32(n_mels))
+        meta[name] = {"n_samples": int(len(pcm)), "n_mels": n_mels, "frames": int(mel.shape[1]),
+                      "pcm_sha256": hashlib.sha256(pcm.tobytes()).hexdigest()}
+        print("mel", name, mel.shape)
+    return meta
+
+
+def build_model(d: D.WhisperDims, w: dict):
+    model = WhisperForConditionalGeneration(hf_config(d)).eval()
+    sd = {k: torch.from_numpy(v) for k, v in weights.to_hf_state_dict(w, d).items()}
+    missing, unexpected = model.load_state_dict(sd, strict=False)
+    missing = [m for m in missing if not m.endswith("k_proj.bias")]
+    assert not missing and not unexpected, (missing, unexpected)
+    return model
+
+
+def gen_tiny(out):
+    d = D.TINY_TEST
+    st = D.SpecialTokens.for_vocab(d.n_vocab)
+    w = weights.random_weights(d, seed=TINY_SEED, emb_std=TINY_EMB_STD)
+    model = build_model(d, w)
+    pcm = synth.chirp_clip(3, 30.0)
+    mel = fe_mel(pcm, d.n_mels)[:, :3000]
+    with torch.no_grad():
+        enc = model.model.encoder(input_features=torch.from_numpy(mel)[None]).last_hidden_state
+    tok = WhisperTokenizer(d.n_vocab)
+    suppress = get_suppressed_tokens(tok, [-1])
+    gc = GenerationConfig(no_timestamps_token_id=st.no_timestamps, eos_token_id=st.eot,
+                          max_initial_timestamp_index=50)
+
+    def step(ids, past):
+        with torch.no_grad():
+            o = model(encoder_outputs=(enc,), decoder_input_ids=torch.tensor([ids]), past_key_values=past,
+                      use_cache=True)
+        return o.logits[0, -1].float(), o.past_key_values
+
+    lg, past = step([st.sot], None)
+    sot_logits = lg.numpy().copy()
+    lang = st.first_lang + int(np.argmax(sot_logits[st.first_lang:st.first_lang + st.n_langs]))
+    nsp = float(torch.softmax(lg.double(), -1)[st.no_speech])
+    prompt = [st.sot, lang, st.transcribe]
+    lg, past = step([lang], past)
+    lg, past = step([st.transcribe], past)
+    begin = len(prompt)
+    procs = [SuppressTokensAtBeginLogitsProcessor([st.blank, st.eot], begin),
+             SuppressTokensLogitsProcessor(list(suppress)),
+             WhisperTimeStampLogitsProcessor(gc, begin)]
+    seq = list(prompt)
+    ids, lps, top5i, top5v, raw = [], [], [], [], []
+    sum_lp = 0.0
+    while True:
+        if len(raw) < 8:
+            raw.append(lg.numpy().copy())
+        x = lg[None].clone()
+        for p in procs:
+            x = p(torch.tensor([seq]), x)
+        lsm = torch.log_softmax(x.double(), -1)[0]
+        nxt = int(torch.argmax(x[0]))
+        v, i = torch.topk(lg, 5)
+        top5i.append(i.numpy())
+        top5v.append(v.numpy())
+        sum_lp += float(lsm[nxt])
+        lps.append(float(lsm[nxt]))
+        if nxt == st.eot:
+            break
+        ids.append(nxt)
+        seq.append(nxt)
+        if len(seq) >= d.n_text_ctx:
+            break
+        lg, past = step([nxt], past)
+    np.savez_compressed(os.path.join(out, "tiny_model.npz"), mel=mel, enc=enc[0].numpy().astype(np.float16),
+                        sot_logits=sot_logits, step_logits=np.stack(raw), ids=np.array(ids, np.int32),
+                        logprobs=np.array(lps), top5_ids=np.stack(top5i).astype(np.int32),
+                        top5_vals=np.stack(top5v), language=np.int32(lang), no_speech_prob=np.float64(nsp),
+                        sum_logprob=np.float64(sum_lp))
+    print("tiny: lang", lang, "n_ids", len(ids), "first", ids[:12])
+    return {"seed": TINY_SEED, "emb_std": TINY_EMB_STD, "language": lang, "n_ids": len(ids)}
+
+
+def gen_turbo_layer(out):
+    """Encoder layer 0 at whisper-large-v3-turbo dims (fp32, transformers)."""
+    d = D.LARGE_V3_TURBO
+    specs = weights.canonical_specs(d)
+    idx = {s.name: i for i, s in enumerate(specs)}
+    w = {}
+    for nm in ("ln1.g", "ln1.b", "qkv.w", "qkv.b", "o.w", "o.b", "ln2.g", "ln2.b", "fc1.w", "fc1.b",
+               "fc2.w", "fc2.b"):
+        full = "enc.l0." + nm
+        w[full] = weights.make_tensor(specs[idx[full]], d, TURBO_LAYER_SEED, idx[full])
+    x = weights.hash_uniform(4242, 0, 1500 * 1280, 1.0, 0.0).reshape(1500, 1280)
+    from transformers.models.whisper.modeling_whisper import WhisperEncoderLayer
+    layer = WhisperEncoderLayer(hf_config(d)).eval()
+    De = d.n_audio_state
+    f = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32))  # noqa: E731
+    with torch.no_grad():
+        sa = layer.self_attn
+        qkv, b = w["enc.l0.qkv.w"], w["enc.l0.qkv.b"]
+        sa.q_proj.weight.copy_(f(qkv[:De])); sa.q_proj.bias.copy_(f(b[:De]))
+        sa.k_proj.weight.copy_(f(qkv[De:2 * De]))
+        sa.v_proj.weight.copy_(f(qkv[2 * De:])); sa.v_proj.bias.copy_(f(b[2 * De:]))
+        sa.out_proj.weight.copy_(f(w["enc.l0.o.w"])); sa.out_proj.bias.copy_(f(w["enc.l0.o.b"]))
+        layer.self_attn_layer_norm.weight.copy_(f(w["enc.l0.ln1.g"]))
+        layer.self_attn_layer_norm.bias.copy_(f(w["enc.l0.ln1.b"]))
+        layer.final_layer_norm.weight.copy_(f(w["enc.l0.ln2.g"]))
+        layer.final_layer_norm.bias.copy_(f(w["enc.l0.ln2.b"]))
+        layer.fc1.weight.copy_(f(w["enc.l0.fc1.w"])); layer.fc1.bias.copy_(f(w["enc.l0.fc1.b"]))
+        layer.fc2.weight.copy_(f(w["enc.l0.fc2.w"])); layer.fc2.bias.copy_(f(w["enc.l0.fc2.b"]))
+        y = layer(torch.from_numpy(x)[None], attention_mask=None)
+        y = (y[0] if isinstance(y, tuple) else y)[0].numpy()
+    rows = np.r_[0:48, 700:716, 1452:1500]
+    np.savez_compressed(os.path.join(out, "turbo_enc_layer0.npz"), rows=rows, y_rows=y[rows].astype(np.float32),
+                        y_rownorm=np.linalg.norm(y.astype(np.float64), axis=1), x_seed=np.int32(4242),
+                        w_seed=np.int32(TURBO_LAYER_SEED))
+    print("turbo layer: |y| mean", float(np.abs(y).mean()))
+    return {"w_seed": TURBO_LAYER_SEED, "x_seed": 4242}
+
+
+def gen_logits_rules(out):
+    """Crafted token histories through transformers' Whisper processors."""
+    st = D.SpecialTokens.for_vocab(51866)
+    tok = WhisperTokenizer(51866)
+    suppress = get_suppressed_tokens(tok, [-1])
+    gc = GenerationConfig(no_timestamps_token_id=st.no_timestamps, eos_token_id=st.eot,
+                          max_initial_timestamp_index=50)
+    tb = st.timestamp_begin
+    cases = [
+        [],                                   # first step: timestamps only, <= 1.00 s
+        [tb + 3],                             # after an opening timestamp
+        [tb + 3, 400, 500],                   # text after timestamp
+        [tb + 3, 400, tb + 40],               # closing timestamp -> pair rule
+        [tb + 3, 400, tb + 40, tb + 40],      # two timestamps -> must be text
+        [tb, 11, 12, tb + 7, tb + 7, 99],     # monotonic timestamps
+        [1000, 2000, 3000],                   # no timestamps so far
+        [tb + 1500],                          # last timestamp
+    ]
+    prompt = [st.sot, st.first_lang, st.transcribe]
+    begin = len(prompt)
+    procs = [SuppressTokensAtBeginLogitsProcessor([st.blank, st.eot], begin),
+             SuppressTokensLogitsProcessor(list(suppress)),
+             WhisperTimeStampLogitsProcessor(gc, begin)]
+    masks, argmaxes, lens, flat = [], [], [], []
+    for ci, hist in enumerate(cases):
+        for variant in range(2):
+            rng = np.random.default_rng(100 + 2 * ci + variant)
+            lg = rng.standard_normal(51866).astype(np.float32) * 2.0
+            if variant == 1:   # make timestamps likely to win the mass rule
+                lg[tb:] += 4.0
+            x = torch.from_numpy(lg)[None]
+            seq = torch.tensor([prompt + hist])
+            for p in procs:
+                x = p(seq, x)
+            masks.append(np.packbits(~torch.isfinite(x[0]).numpy()))
+            argmaxes.append(int(torch.argmax(x[0])))
+            lens.append(len(hist))
+            flat.extend(hist)
+    np.savez_compressed(os.path.join(out, "logits_rules.npz"), masks=np.stack(masks),
+                        argmax=np.array(argmaxes, np.int32), hist_len=np.array(lens, np.int32),
+                        hist=np.array(flat, np.int32), suppress=np.array(suppress, np.int32))
+    return {"n_cases": len(masks)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.join(ROOT, "tests", "golden"))
+    a = ap.parse_args()
+    os.makedirs(a.out, exist_ok=True)
+    torch.manual_seed(0)
+    meta = {"generator": "tools/make_golden.py", "transformers": __import__("transformers").__version__,
+            "torch": torch.__version__}
+    meta["mel"] = gen_mel(a.out)
+    meta["logits_rules"] = gen_logits_rules(a.out)
+    meta["tiny"] = gen_tiny(a.out)
+    meta["turbo_layer"] = gen_turbo_layer(a.out)
+    with open(os.path.join(a.out, "meta.json"), "w") as fh:
+        json.dump(meta, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,230 @@
+#!/usr/bin/env python3
+"""Throughput bench: whisper-large-v3-turbo transcription on MI355X.
+
+A "step" = one pass of the hot path (log-mel -> encoder -> cross-K/V -> greedy
+decode with Whisper's logits rules) over one batch of `--batch` synthetic 30 s
+16 kHz clips per GPU (BASELINE.json configs[2]; configs[3] is the same per-GPU shard
+at N=8).  With N>1 ranks (torchrun, one process per GPU) rank 0 holds every clip
+in HBM and the step starts with an RCCL scatter of the int16 PCM and ends with an
+RCCL gather of the token ids.
+
+Prints ONE JSON line (rank 0).  value = audio seconds transcribed per wall second
+over all ranks (max-over-ranks time).  Weights are random (no checkpoint is
+available offline) and decoding runs to <|endoftext|> or max_length, so tokens
+per clip are reported beside the number.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import osw_path  # noqa: E402
+
+osw_path.load()
+from open_speech_amd import dims as D  # noqa: E402
+from open_speech_amd import synth  # noqa: E402
+from open_speech_amd.engine import DecodeConfig, WhisperEngine  # noqa: E402
+from open_speech_amd.tokenizer import WhisperTokenizer, get_suppressed_tokens  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0        # MI355X spec (MI355X_MICROARCH.md)
+MFMA_F16_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=64, help="30 s clips per GPU per step")
+    ap.add_argument("--model", default="large-v3-turbo", choices=sorted(D.PRESETS))
+    ap.add_argument("--max-length", type=int, default=448)
+    ap.add_argument("--latency-repeats", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-decode-steps", type=int, default=8)
+    return ap.parse_args()
+
+
+def make_clips(n: int, offset: int = 0, unique: int = 32) -> np.ndarray:
+    """n synthetic clips; at most `unique` distinct ones (cycled) to bound host time."""
+    base = [synth.chirp_clip(offset + i, 30.0) for i in range(min(n, unique))]
+    return np.stack([base[i % len(base)] for i in range(n)])
+
+
+def cpu_baseline(dims, n_tokens_per_clip: float, decode_steps: int) -> dict:
+    """The oracle (numpy restatement, fp32) on the host cores: one clip's log-mel +
+    encoder + `decode_steps` decoder steps, scaled to audio-s/s with the GPU run's
+    tokens per clip.  Test infrastructure used only as the reported CPU baseline."""
+    from oracle import mel as omel
+    from oracle.model import WhisperOracle
+    from open_speech_amd import weights
+
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max((i.get("num_threads", 1) for i in threadpool_info()), default=1)
+    except Exception:
+        cores = os.cpu_count() or 1
+    w = weights.random_weights(dims, seed=0)
+    orc = WhisperOracle(dims, w, fp16=False)
+    del w
+    st = D.SpecialTokens.for_vocab(dims.n_vocab)
+    pcm = synth.chirp_clip(0, 30.0)
+    t0 = time.perf_counter()
+    mel = omel.log_mel(omel.pcm16_to_float(pcm), dims.n_mels)
+    t1 = time.perf_counter()
+    enc = orc.encode(mel[:, :3000].astype(np.float32))
+    xkv = orc.cross_kv(enc)
+    t2 = time.perf_counter()
+    cache = orc.new_cache()
+    toks = [st.sot, st.first_lang, st.transcribe] + [st.timestamp_begin] * max(0, decode_steps - 3)
+    for p, t in enumerate(toks[:decode_steps]):
+        orc.decoder_step(t, p, cache, xkv)
+    t3 = time.perf_counter()
+    per_step = (t3 - t2) / max(1, decode_steps)
+    per_clip = (t1 - t0) + (t2 - t1) + per_step * (3 + n_tokens_per_clip)
+    return {"value": round(30.0 / per_clip, 4), "unit": "audio-sec/sec", "cores": int(cores), "kind": "port",
+            "sample": f"oracle (numpy fp32) on 1 x 30 s clip: log-mel {t1 - t0:.2f}s + encoder+crossKV "
+                      f"{t2 - t1:.2f}s + {decode_steps} decoder steps ({per_step * 1e3:.0f} ms/step), scaled to "
+                      f"{3 + n_tokens_per_clip:.0f} decoder steps per clip (the GPU run's mean)"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+    dims = D.PRESETS[a.model]
+    B = a.batch
+    eng = WhisperEngine(dims, device=dev.index, max_batch=B)
+    eng.init_random(seed=0)
+    sup = get_suppressed_tokens(WhisperTokenizer(dims.n_vocab), [-1])
+    cfg = DecodeConfig(suppress_tokens=sup, max_length=a.max_length)
+
+    n_total = B * world
+    # inputs resident in HBM: rank 0 holds every clip (int16 bytes carried as fp16 for RCCL)
+    if rank == 0:
+        allpcm = torch.from_numpy(make_clips(n_total)).to(dev)
+    shard = torch.empty((B, 480000), dtype=torch.int16, device=dev)
+    offsets = np.arange(B + 1, dtype=np.int64) * 480000
+    tok_dev = torch.empty((B, dims.n_text_ctx), dtype=torch.int32, device=dev)
+
+    def step():
+        if world > 1:
+            chunks = list(allpcm.view(torch.float16).chunk(world)) if rank == 0 else None
+            dist.scatter(shard.view(torch.float16), chunks, src=0)
+        else:
+            shard.copy_(allpcm)
+        torch.cuda.synchronize(dev)
+        outs = eng.transcribe_batch(None, cfg, device_pcm=shard.data_ptr(), offsets=offsets)
+        if world > 1:
+            t = np.full((B, dims.n_text_ctx), -1, np.int32)
+            for i, o in enumerate(outs):
+                t[i, :len(o.tokens)] = o.tokens
+            tok_dev.copy_(torch.from_numpy(t))
+            gl = [torch.empty_like(tok_dev) for _ in range(world)] if rank == 0 else None
+            dist.gather(tok_dev, gl, dst=0)
+        return outs
+
+    for _ in range(a.warmup):
+        step()
+    eng.set_profiling(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ntok = 0
+    for _ in range(a.steps):
+        outs = step()
+        ntok += sum(len(o.tokens) for o in outs)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    prof = eng.profile()
+    eng.set_profiling(False)
+    if dist:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        nt = torch.tensor([ntok], dtype=torch.float64, device=dev)
+        dist.all_reduce(nt)
+        ntok = int(nt.item())
+
+    audio_s = n_total * a.steps * 30.0
+    value = audio_s / el
+    tokens_per_clip = ntok / (n_total * a.steps)
+
+    if rank == 0:
+        # dominant kernel over the timed region (HIP events on the library's stream)
+        cands = {
+            "encoder_gemm": (prof["enc_gemm_ms"], prof["enc_gemm_flops"], prof["enc_gemm_launches"], "mfma"),
+            "encoder_attention": (prof["enc_attn_ms"], prof["enc_attn_flops"], prof["enc_attn_launches"], "mfma"),
+            "decoder_cross_attention": (prof["xattn_ms"], prof["xattn_bytes"], prof["xattn_launches"], "hbm"),
+            "log_mel": (prof["mel_kernel_ms"], prof["mel_kernel_bytes"], prof["mel_kernel_launches"], "hbm"),
+        }
+        name, (ms, work, nl, bound) = max(cands.items(), key=lambda kv: kv[1][0])
+        if bound == "mfma":
+            ach = work / (ms * 1e-3) / 1e12
+            roof = {"kernel": name, "bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_F16_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(ach / MFMA_F16_PEAK_TFLOPS, 4), "traffic": None}
+        else:
+            ach = work / (ms * 1e-3) / 1e9
+            roof = {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
+        roof["avg_launch_ms"] = round(ms / max(1, nl), 4)
+        stages = {k: {"ms": round(v[0], 2), "launches": int(v[2])} for k, v in cands.items()}
+
+        # p50 latency at batch 1 (BASELINE configs[1])
+        lat = []
+        one = torch.from_numpy(make_clips(1, offset=999)).to(dev)
+        for _ in range(a.latency_repeats):
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            eng.transcribe_batch(None, cfg, device_pcm=one.data_ptr(), offsets=np.array([0, 480000], np.int64))
+            lat.append((time.perf_counter() - t1) * 1e3)
+        p50 = float(np.median(lat)) if lat else None
+
+        cpu = None
+        if not a.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(dims, tokens_per_clip, a.cpu_decode_steps)
+
+        line = {
+            "metric": "audio-sec/sec (whisper-large-v3-turbo, 30 s clips, greedy)",
+            "value": round(value, 2), "unit": "audio-sec/sec", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f16", "data": "synthetic (chirps+noise, random weights)",
+            "config": {"workload": f"{a.model}: {B} x 30 s clips per GPU per step, mel+encoder+greedy decode "
+                                   f"(max_length {a.max_length})" + (", RCCL scatter/gather" if world > 1 else ""),
+                       "clips_per_gpu": B, "global_batch": n_total, "parallelism": f"dp{world}"},
+            "tokens_per_clip": round(tokens_per_clip, 1),
+            "p50_latency_ms_b1": None if p50 is None else round(p50, 2),
+            "realtime_factor": round(value, 1),
+            "roofline": roof,
+            "stages_ms": stages,
+            "decode_steps_last_call": int(prof["decode_steps"]),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,141 @@
+/*
+ * osw.h — C ABI of libosw_hip.so, the MI355X (gfx950) Whisper transcription engine.
+ *
+ * This library is the drop-in for the arithmetic the reference delegates to
+ * faster-whisper 1.2.1 / CTranslate2.  Each entry point names the reference
+ * interface it replaces (paths under the reference repository):
+ *
+ *   osw_create / osw_set_weight / osw_init_weight_uniform / osw_finalize
+ *       replace   WhisperModel(model_id, device, compute_type, download_root)
+ *                 called at src/backends/faster_whisper.py:40-45 (load_model :29-50)
+ *   osw_destroy
+ *       replaces  del self._models[model_id]; gc; empty_cache   (unload_model :52-65)
+ *   osw_transcribe_batch
+ *       replaces  WhisperModel.transcribe(path, task, beam_size, temperature,
+ *                 language, initial_prompt) + list(segments)     (:235-246),
+ *                 for the first 30 s window of every clip (greedy, beam_size = 1)
+ *   osw_log_mel / osw_encode_windows / osw_decode_windows
+ *       the same work split by stage, as faster-whisper's generate_segments seek
+ *       loop needs it (FeatureExtractor -> encode -> generate per 30 s window)
+ *   osw_get_mel / osw_get_encoder_output / osw_encoder_layer_debug
+ *       stage-level read-back used only by the parity tests
+ *
+ * Conventions: every call returns 0 (OSW_OK) or a negative code; the message of
+ * the last failure on the calling thread is osw_last_error().  Host buffers are
+ * caller-owned and only read/written during the call (the library copies them).
+ * A context serialises its own calls (internal mutex); one context per device.
+ * No torch types cross this boundary.
+ */
+#ifndef OSW_H
+#define OSW_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OSW_OK 0
+#define OSW_EINVAL (-22)
+#define OSW_ENOMEM (-12)
+#define OSW_EHIP (-100)
+#define OSW_ESTATE (-101)
+
+typedef struct osw_ctx osw_ctx;
+
+typedef struct osw_dims {
+    int32_t n_mels, n_audio_ctx, n_audio_state, n_audio_head, n_audio_layer;
+    int32_t n_vocab, n_text_ctx, n_text_state, n_text_head, n_text_layer;
+} osw_dims;
+
+/* One 30 s decoding window: frames [seek, seek + segment_size) of clip `clip`'s
+ * log-mel, zero padded to 3000 frames (faster-whisper pad_or_trim). */
+typedef struct osw_window {
+    int32_t clip;
+    int32_t seek;
+    int32_t segment_size;
+} osw_window;
+
+typedef struct osw_decode_opts {
+    int32_t task_token;          /* <|transcribe|> or <|translate|> */
+    int32_t language_token;      /* -1: detect from the <|startoftranscript|> logits */
+    int32_t suppress_blank;      /* suppress " " and <|endoftext|> at the first sampled step */
+    int32_t without_timestamps;  /* 0: timestamp rules on (faster-whisper default) */
+    int32_t max_initial_timestamp_index; /* 50 = 1.0 s; -1 disables */
+    int32_t max_length;          /* total positions (prompt + sampled), <= n_text_ctx */
+    const int32_t* suppress_tokens; int32_t n_suppress;
+    /* special token ids */
+    int32_t eot, sot, sot_prev, no_speech, no_timestamps, timestamp_begin, blank;
+    int32_t first_lang, n_langs;
+    /* tokens placed BEFORE <|startoftranscript|> (e.g. <|startofprev|> + previous
+     * text), n_windows * n_prefix ints, same length for every window of the call */
+    const int32_t* prefix_tokens; int32_t n_prefix;
+} osw_decode_opts;
+
+/* Caller-allocated outputs for n windows. */
+typedef struct osw_window_result {
+    int32_t* tokens;          /* [n][max_tokens]: sampled tokens (no prompt, no EOT) */
+    int32_t max_tokens;
+    int32_t* n_tokens;        /* [n] */
+    float* sum_logprob;       /* [n]  includes the EOT step, as CTranslate2 scores do */
+    float* no_speech_prob;    /* [n]  softmax(raw SOT logits)[no_speech] */
+    int32_t* language;        /* [n]  language token used */
+    float* logits_dump;       /* optional [n][dump_steps][n_vocab] raw logits of the first sampled steps */
+    int32_t dump_steps;
+} osw_window_result;
+
+typedef struct osw_profile {
+    double mel_ms, encoder_ms, crosskv_ms, decoder_ms, total_ms;
+    int64_t decode_steps;           /* decoder steps launched in the last decode call */
+    /* dominant-kernel accounting (HIP events around every launch of the class) */
+    double enc_gemm_ms; int64_t enc_gemm_launches; double enc_gemm_flops;
+    double enc_attn_ms; int64_t enc_attn_launches; double enc_attn_flops;
+    double mel_kernel_ms; int64_t mel_kernel_launches; double mel_kernel_bytes;
+    double xattn_ms; int64_t xattn_launches; double xattn_bytes;
+} osw_profile;
+
+const char* osw_version(void);
+const char* osw_last_error(void);
+int osw_device_count(int32_t* out);
+
+int osw_create(const osw_dims* dims, int32_t device, int32_t max_batch, osw_ctx** out);
+int osw_destroy(osw_ctx* ctx);
+
+/* Upload one canonical tensor (names and dtypes: open-speech_amd/weights.py). */
+int osw_set_weight(osw_ctx* ctx, const char* name, const void* host, int64_t nbytes);
+/* Device-side counter-hash init: x[i] = (2u-1)*scale + offset, u from splitmix64. */
+int osw_init_weight_uniform(osw_ctx* ctx, const char* name, uint64_t seed, int64_t stream,
+                            float scale, float offset, int64_t zero_lo, int64_t zero_hi);
+int osw_finalize(osw_ctx* ctx);   /* all tensors present? derive internal layouts */
+
+/* PCM int16 of n_clips clips, clip i = pcm[offsets[i], offsets[i+1]).  When
+ * pcm_on_device != 0, `pcm` is a device pointer on the context's device.
+ * Computes the faster-whisper log-mel (padding 160, per-clip max clamp) and keeps it
+ * resident; n_frames[i] receives the frame count of clip i. */
+int osw_log_mel(osw_ctx* ctx, const int16_t* pcm, const int64_t* offsets, int32_t n_clips,
+                int32_t pcm_on_device, int32_t* n_frames);
+int osw_get_mel(osw_ctx* ctx, int32_t clip, float* out, int64_t out_floats);  /* [n_mels][n_frames] */
+
+/* Encoder + cross-attention K/V for n windows of the resident log-mel. */
+int osw_encode_windows(osw_ctx* ctx, const osw_window* windows, int32_t n);
+int osw_get_encoder_output(osw_ctx* ctx, int32_t window, float* out, int64_t out_floats); /* [1500][D] */
+
+/* Greedy decode of the n windows last encoded. */
+int osw_decode_windows(osw_ctx* ctx, int32_t n, const osw_decode_opts* opts, osw_window_result* res);
+
+/* mel + encode + greedy decode of window 0 (seek 0, min(frames, 3000)) of every clip. */
+int osw_transcribe_batch(osw_ctx* ctx, const int16_t* pcm, const int64_t* offsets, int32_t n_clips,
+                         int32_t pcm_on_device, const osw_decode_opts* opts, osw_window_result* res);
+
+/* Parity helper: one encoder block on x [T][D] fp32 (host), result to y (host). */
+int osw_encoder_layer_debug(osw_ctx* ctx, int32_t layer, const float* x, float* y, int32_t T);
+
+int osw_set_profiling(osw_ctx* ctx, int32_t enable);
+int osw_get_profile(osw_ctx* ctx, osw_profile* out);
+/* Device stream used by the context (hipStream_t as void*). */
+void* osw_stream(osw_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OSW_H */

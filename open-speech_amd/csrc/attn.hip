@@ -1,0 +1,204 @@
+// Encoder self-attention (non-causal, T = 1500, head_dim 64) for gfx950.
+//
+// Flash-style: one workgroup = 4 waves = 128 queries of one (window, head); each
+// wave owns 32 queries (two 16-query MFMA tiles).  K/V tiles of 64 keys are staged
+// global -> LDS by 16-byte global_load_lds (double buffered; the 16-B chunk is
+// XOR-swizzled through the source address as in gemm.hip).
+//
+//   Sᵀ = K · Qᵀ      v_mfma_f32_16x16x32_f16, A = K rows (ds_read_b128), B = Q (registers)
+//                    -> each lane holds 16 scores of ONE query (lane & 15): the row
+//                       max/sum need only 2 cross-lane xor-shuffles (16, 32)
+//   Oᵀ += Vᵀ · Pᵀ    A = V read with ds_read_b64_tr_b16 (hardware transpose), B = P
+//                    straight from the score registers (same k permutation on both
+//                    operands), so O's query is again lane & 15 and the online-softmax
+//                    rescale is lane-local.
+// Softmax in fp32 base-2 with the 1/sqrt(64)·log2(e) scale folded into one multiply;
+// P is rounded to fp16 for the PV MFMA (the oracle emulates exactly that).
+//
+// Layout in:  QKV head-major [3][nb][H][T][64] fp16 (written by the QKV GEMM epilogue)
+// Layout out: O [nb*T][H*64] fp16 row-major (the out-projection GEMM's A operand)
+#include "common.h"
+
+namespace osw {
+
+namespace {
+constexpr int QB = 128, KB = 64, HD = 64;
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+typedef __fp16 fp16x4_t __attribute__((__vector_size__(4 * sizeof(__fp16))));
+
+__device__ __forceinline__ h16x4 ds_read_tr(const h16* p) {
+    fp16x4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4f16((OSW_LDS fp16x4_t*)p);
+    return __builtin_bit_cast(h16x4, v);
+}
+
+__global__ __launch_bounds__(256, 2) void enc_attn_kernel(const h16* __restrict__ qkv, h16* __restrict__ out,
+                                                          int T, int H, int nb) {
+    __shared__ __attribute__((aligned(16))) h16 lds[2][2][KB * HD];  // [buf][K|V] 32 KiB
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int g = lane >> 4, li = lane & 15;
+    const int h = blockIdx.y, b = blockIdx.z;
+    const int q0 = blockIdx.x * QB + wave * 32;
+    const int64_t head_elems = (int64_t)T * HD;
+    const h16* Qh = qkv + (((int64_t)0 * nb + b) * H + h) * head_elems;
+    const h16* Kh = qkv + (((int64_t)1 * nb + b) * H + h) * head_elems;
+    const h16* Vh = qkv + (((int64_t)2 * nb + b) * H + h) * head_elems;
+
+    // Q fragments (B operand): lane: q = q0 + qt*16 + li, d = 32 s + 8 g + j
+    h16x8 qf[2][2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+        const int q = min(q0 + qt * 16 + li, T - 1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) qf[qt][s] = *(const h16x8*)(Qh + (int64_t)q * HD + 32 * s + 8 * g);
+    }
+
+    // glds pieces: 64 rows x 128 B = 8 KiB per tile = 8 wave-instructions; K: 2 per wave, V: 2 per wave
+    auto stage = [&](int buf, int k0) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int piece = i * 4 + wave;           // rows piece*8 .. +7
+            const int r = piece * 8 + (lane >> 3);
+            const int c = swz(r, lane & 7);
+            const int key = min(k0 + r, T - 1);
+            __builtin_amdgcn_global_load_lds((const void*)(Kh + (int64_t)key * HD + c * 8),
+                                             (OSW_LDS void*)&lds[buf][0][piece * 8 * HD], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)(Vh + (int64_t)key * HD + c * 8),
+                                             (OSW_LDS void*)&lds[buf][1][piece * 8 * HD], 16, 0, 0);
+        }
+    };
+
+    const float cs = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
+    float mrun[2] = {-INFINITY, -INFINITY};
+    float lrun[2] = {0.f, 0.f};
+    f32x4 o[2][4];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[qt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nkt = (T + KB - 1) / KB;
+    stage(0, 0);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nkt) stage(buf ^ 1, (kt + 1) * KB);
+        const h16* Kl = lds[buf][0];
+        const h16* Vl = lds[buf][1];
+        const int k0 = kt * KB;
+
+        // ---- Sᵀ = K Qᵀ : sc[qt][t] holds keys 16t + 4g + i for query li
+        f32x4 sc[2][4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int row = 16 * t + li;
+            const h16x8 k0f = *(const h16x8*)&Kl[row * HD + swz(row, g) * 8];
+            const h16x8 k1f = *(const h16x8*)&Kl[row * HD + swz(row, 4 + g) * 8];
+#pragma unroll
+            for (int qt = 0; qt < 2; ++qt) {
+                f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(k0f, qf[qt][0], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(k1f, qf[qt][1], a, 0, 0, 0);
+                sc[qt][t] = a;
+            }
+        }
+        // ---- online softmax (lane-local per query; 4 lanes g=0..3 share a query)
+        h16x8 pf[2][2];
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+            float mx = -INFINITY;
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int key = k0 + 16 * t + 4 * g + i;
+                    float v = sc[qt][t][i] * cs;
+                    v = key < T ? v : -INFINITY;
+                    sc[qt][t][i] = v;
+                    mx = fmaxf(mx, v);
+                }
+            mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            const float mnew = fmaxf(mrun[qt], mx);
+            const float alpha = exp2f(mrun[qt] - mnew);
+            mrun[qt] = mnew;
+            float ls = 0.f;
+            float p[4][4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    p[t][i] = exp2f(sc[qt][t][i] - mnew);
+                    ls += p[t][i];
+                }
+            lrun[qt] = lrun[qt] * alpha + ls;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) o[qt][dt] *= alpha;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                h16x8 f;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    f[j] = (h16)p[2 * s][j];
+                    f[4 + j] = (h16)p[2 * s + 1][j];
+                }
+                pf[qt][s] = f;
+            }
+        }
+        // ---- Oᵀ += Vᵀ Pᵀ ; A = V via transposed LDS reads
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                const int q4 = li >> 2, p4 = li & 3;
+                const int col = 16 * dt + 4 * p4;
+                const int ch = col >> 3, within = col & 7;
+                const int r0 = 32 * s + 4 * g + q4;
+                const int r1 = r0 + 16;
+                const h16x4 va = ds_read_tr(&Vl[r0 * HD + swz(r0, ch) * 8 + within]);
+                const h16x4 vb = ds_read_tr(&Vl[r1 * HD + swz(r1, ch) * 8 + within]);
+                h16x8 vf;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    vf[j] = va[j];
+                    vf[4 + j] = vb[j];
+                }
+#pragma unroll
+                for (int qt = 0; qt < 2; ++qt)
+                    o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf[qt][s], o[qt][dt], 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+    }
+
+    // ---- normalise and store: lane holds O[q = li][d = 16 dt + 4 g + i]
+    const int D = H * HD;
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+        float l = lrun[qt];
+        l += __shfl_xor(l, 16, 64);
+        l += __shfl_xor(l, 32, 64);
+        const float inv = 1.0f / l;
+        const int q = q0 + qt * 16 + li;
+        if (q >= T) continue;
+        h16* orow = out + ((int64_t)b * T + q) * D + h * HD;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+            h16x4 v;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = (h16)(o[qt][dt][i] * inv);
+            *(h16x4*)(orow + 16 * dt + 4 * g) = v;
+        }
+    }
+}
+}  // namespace
+
+void launch_enc_attn(const h16* qkv, h16* out, int T, int H, int nb, hipStream_t s) {
+    dim3 grid((T + QB - 1) / QB, H, nb);
+    enc_attn_kernel<<<grid, 256, 0, s>>>(qkv, out, T, H, nb);
+}
+
+}  // namespace osw

@@ -1,0 +1,979 @@
+// libosw_hip.so runtime: context, weights, resident buffers, encoder / decoder
+// pipelines and the C ABI of include/osw.h.
+//
+// One context = one device, one HIP stream, buffers sized for `max_batch` windows
+// at creation (nothing is allocated in the per-call hot path except when a call
+// brings more PCM / mel than any earlier call).  Calls on one context are
+// serialised by a mutex; independent contexts (one per GPU) run concurrently.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/osw.h"
+#include "common.h"
+
+namespace osw {
+// launchers from the other translation units
+void launch_mel(const int16_t*, const int64_t*, const int64_t*, const int*, int, int, const float2*, const float*,
+                const int*, const int*, const int*, const float*, int, float*, int*, hipStream_t);
+void launch_mel_window(const float*, const int64_t*, const int*, const int*, const int*, const int*, const int*, int,
+                       int, int, h16*, hipStream_t);
+void launch_mel_normalize(const float*, int64_t, int, int, const int*, int, float*, hipStream_t);
+void launch_enc_attn(const h16*, h16*, int, int, int, hipStream_t);
+void launch_init_uniform(void*, bool, int64_t, uint64_t, float, float, int64_t, int64_t, hipStream_t);
+uint64_t hash_stream_key(uint64_t, int64_t);
+void launch_dec_embed(const h16*, const float*, const int*, const int*, int, int, int, float*, hipStream_t);
+void launch_dec_self_attn(const h16*, h16*, h16*, const int*, int, int, int, h16*, hipStream_t);
+void launch_dec_cross_attn(const h16*, const h16*, const h16*, int, int, int, h16*, hipStream_t);
+void launch_select(const float*, int, const int*, int, int, int, int, int, int, int, int, int, int, int, int, int, int,
+                   int, const int*, const unsigned*, void*, int*, int*, int, hipStream_t);
+void launch_count_done(const void*, int, int*, hipStream_t);
+void launch_bump(int*, hipStream_t);
+int sel_state_bytes();
+}  // namespace osw
+
+using namespace osw;
+
+namespace {
+thread_local std::string g_err;
+
+struct OswError : std::runtime_error {
+    int code;
+    OswError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIPCHK(x)                                                                                  \
+    do {                                                                                           \
+        hipError_t e_ = (x);                                                                       \
+        if (e_ != hipSuccess)                                                                      \
+            throw OswError(OSW_EHIP, std::string(#x) + ": " + hipGetErrorString(e_) + " @" +       \
+                                         std::to_string(__LINE__));                                \
+    } while (0)
+#define REQUIRE(c, msg) \
+    do {                \
+        if (!(c)) throw OswError(OSW_EINVAL, msg); \
+    } while (0)
+
+template <typename F>
+int guard(F&& f) {
+    try {
+        f();
+        return OSW_OK;
+    } catch (const OswError& e) {
+        g_err = e.what();
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        g_err = "out of host memory";
+        return OSW_ENOMEM;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return OSW_ESTATE;
+    }
+}
+
+struct Tensor {
+    void* ptr = nullptr;
+    int64_t numel = 0;
+    bool f16 = true;
+    bool set = false;
+};
+
+template <typename T>
+T* dalloc(size_t n, std::vector<void*>& owned) {
+    void* p = nullptr;
+    if (n == 0) n = 1;
+    hipError_t e = hipMalloc(&p, n * sizeof(T));
+    if (e != hipSuccess) throw OswError(OSW_ENOMEM, "hipMalloc " + std::to_string(n * sizeof(T)) + " B failed");
+    owned.push_back(p);
+    return (T*)p;
+}
+
+struct EventPair {
+    hipEvent_t a, b;
+    int cls;
+    double work;
+};
+}  // namespace
+
+struct osw_ctx {
+    std::mutex mu;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    osw_dims d{};
+    int B = 0;    // max windows per call
+    int C1 = 0;   // conv1 input channels padded to a multiple of 64
+    std::vector<void*> owned;
+    std::map<std::string, Tensor> w;
+    bool finalized = false;
+
+    // mel constants
+    float2* tw400 = nullptr;
+    float* hann = nullptr;
+    int *flo = nullptr, *fcnt = nullptr, *foff = nullptr;
+    float* fw = nullptr;
+    // resident mel
+    int16_t* pcm = nullptr;
+    size_t pcm_cap = 0;
+    int64_t* offsets = nullptr;
+    int64_t* mel_off_d = nullptr;
+    int* nframes_d = nullptr;
+    int* clip_max = nullptr;
+    int clips_cap = 0;
+    float* logmel = nullptr;
+    size_t logmel_cap = 0;
+    int n_clips = 0;
+    std::vector<int> nframes;
+    std::vector<int64_t> mel_off;
+
+    // encoder workspace
+    int* win = nullptr;  // [3][B]
+    h16 *X1 = nullptr, *H1 = nullptr, *Xn = nullptr, *QKV = nullptr, *O = nullptr, *Hf = nullptr, *E = nullptr,
+        *XKV = nullptr;
+    float* X = nullptr;
+    int n_encoded = 0;
+
+    // decoder workspace
+    float* xd = nullptr;
+    h16 *xdn = nullptr, *dqkv = nullptr, *dattn = nullptr, *dq = nullptr, *dh = nullptr, *kc = nullptr, *vc = nullptr;
+    float* logits = nullptr;
+    int *cur_tok = nullptr, *pos = nullptr, *tokens = nullptr, *prompt = nullptr, *done = nullptr;
+    unsigned* supmask = nullptr;
+    void* sel = nullptr;
+    int* done_host = nullptr;  // pinned
+    float* part = nullptr;     // split-K partial slabs of the decoder GEMMs
+    int64_t part_floats = 0;
+
+    // decode-step graph (CH steps per replay), re-captured when its key changes
+    hipGraphExec_t dgraph = nullptr;
+    std::vector<int64_t> dgraph_key;
+    bool capturing = false;
+    bool use_graph = true;
+
+    // profiling
+    bool prof = false;
+    osw_profile pf{};
+    std::vector<EventPair> evs;
+    std::vector<hipEvent_t> ev_free;
+};
+
+namespace {
+const int T_ENC = 1500;
+const int N_FR = 3000;
+
+hipEvent_t get_ev(osw_ctx* c) {
+    if (!c->ev_free.empty()) {
+        hipEvent_t e = c->ev_free.back();
+        c->ev_free.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    return e;
+}
+
+// class ids for per-launch accounting
+enum { CL_ENC_GEMM = 1, CL_ENC_ATTN = 2, CL_MEL = 3, CL_XATTN = 4, CL_STAGE_MEL = 10, CL_STAGE_ENC = 11,
+       CL_STAGE_XKV = 12, CL_STAGE_DEC = 13 };
+
+struct Timed {
+    osw_ctx* c;
+    EventPair p{};
+    bool on;
+    Timed(osw_ctx* c_, int cls, double work) : c(c_), on(c_->prof && !c_->capturing) {
+        if (!on) return;
+        p.a = get_ev(c);
+        p.b = get_ev(c);
+        p.cls = cls;
+        p.work = work;
+        HIPCHK(hipEventRecord(p.a, c->stream));
+    }
+    ~Timed() {
+        if (!on) return;
+        if (hipEventRecord(p.b, c->stream) == hipSuccess) c->evs.push_back(p);
+    }
+};
+
+void resolve_events(osw_ctx* c) {
+    if (c->evs.empty()) return;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (auto& e : c->evs) {
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, e.a, e.b));
+        osw_profile& p = c->pf;
+        switch (e.cls) {
+            case CL_ENC_GEMM: p.enc_gemm_ms += ms; p.enc_gemm_launches++; p.enc_gemm_flops += e.work; break;
+            case CL_ENC_ATTN: p.enc_attn_ms += ms; p.enc_attn_launches++; p.enc_attn_flops += e.work; break;
+            case CL_MEL: p.mel_kernel_ms += ms; p.mel_kernel_launches++; p.mel_kernel_bytes += e.work; break;
+            case CL_XATTN: p.xattn_ms += ms; p.xattn_launches++; p.xattn_bytes += e.work; break;
+            case CL_STAGE_MEL: p.mel_ms += ms; break;
+            case CL_STAGE_ENC: p.encoder_ms += ms; break;
+            case CL_STAGE_XKV: p.crosskv_ms += ms; break;
+            case CL_STAGE_DEC: p.decoder_ms += ms; break;
+        }
+        c->ev_free.push_back(e.a);
+        c->ev_free.push_back(e.b);
+    }
+    c->evs.clear();
+}
+
+// ---------------------------------------------------------------------------
+void add_tensor(osw_ctx* c, const std::string& name, int64_t numel, bool f16) {
+    Tensor t;
+    t.numel = numel;
+    t.f16 = f16;
+    c->w[name] = t;
+}
+
+void build_weight_table(osw_ctx* c) {
+    const osw_dims& d = c->d;
+    const int64_t De = d.n_audio_state, Dd = d.n_text_state, L = d.n_text_layer;
+    add_tensor(c, "enc.conv1.w", De * 3 * c->C1, true);  // stored padded [De][3][C1]
+    add_tensor(c, "enc.conv1.b", De, false);
+    add_tensor(c, "enc.conv2.w", De * 3 * De, true);
+    add_tensor(c, "enc.conv2.b", De, false);
+    add_tensor(c, "enc.pos", (int64_t)d.n_audio_ctx * De, false);
+    for (int i = 0; i < d.n_audio_layer; ++i) {
+        const std::string p = "enc.l" + std::to_string(i);
+        add_tensor(c, p + ".ln1.g", De, false);
+        add_tensor(c, p + ".ln1.b", De, false);
+        add_tensor(c, p + ".qkv.w", 3 * De * De, true);
+        add_tensor(c, p + ".qkv.b", 3 * De, false);
+        add_tensor(c, p + ".o.w", De * De, true);
+        add_tensor(c, p + ".o.b", De, false);
+        add_tensor(c, p + ".ln2.g", De, false);
+        add_tensor(c, p + ".ln2.b", De, false);
+        add_tensor(c, p + ".fc1.w", 4 * De * De, true);
+        add_tensor(c, p + ".fc1.b", 4 * De, false);
+        add_tensor(c, p + ".fc2.w", 4 * De * De, true);
+        add_tensor(c, p + ".fc2.b", De, false);
+    }
+    add_tensor(c, "enc.lnpost.g", De, false);
+    add_tensor(c, "enc.lnpost.b", De, false);
+    add_tensor(c, "dec.tok", (int64_t)d.n_vocab * Dd, true);
+    add_tensor(c, "dec.pos", (int64_t)d.n_text_ctx * Dd, false);
+    add_tensor(c, "dec.crosskv.w", L * 2 * Dd * De, true);
+    add_tensor(c, "dec.crosskv.b", L * 2 * Dd, false);
+    for (int i = 0; i < d.n_text_layer; ++i) {
+        const std::string p = "dec.l" + std::to_string(i);
+        add_tensor(c, p + ".ln1.g", Dd, false);
+        add_tensor(c, p + ".ln1.b", Dd, false);
+        add_tensor(c, p + ".qkv.w", 3 * Dd * Dd, true);
+        add_tensor(c, p + ".qkv.b", 3 * Dd, false);
+        add_tensor(c, p + ".o.w", Dd * Dd, true);
+        add_tensor(c, p + ".o.b", Dd, false);
+        add_tensor(c, p + ".ln2.g", Dd, false);
+        add_tensor(c, p + ".ln2.b", Dd, false);
+        add_tensor(c, p + ".xq.w", Dd * Dd, true);
+        add_tensor(c, p + ".xq.b", Dd, false);
+        add_tensor(c, p + ".xo.w", Dd * Dd, true);
+        add_tensor(c, p + ".xo.b", Dd, false);
+        add_tensor(c, p + ".ln3.g", Dd, false);
+        add_tensor(c, p + ".ln3.b", Dd, false);
+        add_tensor(c, p + ".fc1.w", 4 * Dd * Dd, true);
+        add_tensor(c, p + ".fc1.b", 4 * Dd, false);
+        add_tensor(c, p + ".fc2.w", 4 * Dd * Dd, true);
+        add_tensor(c, p + ".fc2.b", Dd, false);
+    }
+    add_tensor(c, "dec.lnpost.g", Dd, false);
+    add_tensor(c, "dec.lnpost.b", Dd, false);
+
+    // one arena, every tensor 256-B aligned
+    size_t total = 0;
+    for (auto& kv : c->w) total += ((size_t)kv.second.numel * (kv.second.f16 ? 2 : 4) + 255) & ~(size_t)255;
+    char* arena = dalloc<char>(total, c->owned);
+    HIPCHK(hipMemsetAsync(arena, 0, total, c->stream));
+    size_t off = 0;
+    for (auto& kv : c->w) {
+        kv.second.ptr = arena + off;
+        off += ((size_t)kv.second.numel * (kv.second.f16 ? 2 : 4) + 255) & ~(size_t)255;
+    }
+}
+
+Tensor& W(osw_ctx* c, const std::string& n) {
+    auto it = c->w.find(n);
+    if (it == c->w.end()) throw OswError(OSW_EINVAL, "unknown tensor " + n);
+    return it->second;
+}
+const h16* WH(osw_ctx* c, const std::string& n) { return (const h16*)W(c, n).ptr; }
+const float* WF(osw_ctx* c, const std::string& n) { return (const float*)W(c, n).ptr; }
+
+// --------------------------- mel constants ---------------------------------
+double hz_to_mel(double f) {
+    const double f_sp = 200.0 / 3, min_log_hz = 1000.0, min_log_mel = min_log_hz / f_sp, logstep = std::log(6.4) / 27.0;
+    return f >= min_log_hz ? min_log_mel + std::log(f / min_log_hz) / logstep : f / f_sp;
+}
+double mel_to_hz(double m) {
+    const double f_sp = 200.0 / 3, min_log_hz = 1000.0, min_log_mel = min_log_hz / f_sp, logstep = std::log(6.4) / 27.0;
+    return m >= min_log_mel ? min_log_hz * std::exp(logstep * (m - min_log_mel)) : f_sp * m;
+}
+
+void setup_mel(osw_ctx* c) {
+    const int n_mels = c->d.n_mels;
+    std::vector<float2> tw(400);
+    std::vector<float> hn(400);
+    for (int j = 0; j < 400; ++j) {
+        const double a = 2.0 * M_PI * j / 400.0;
+        tw[j] = make_float2((float)std::cos(a), (float)-std::sin(a));
+        hn[j] = (float)(0.5 - 0.5 * std::cos(a));
+    }
+    // slaney mel bank (librosa / faster-whisper get_mel_filters), double precision
+    std::vector<double> mel_f(n_mels + 2);
+    const double mmin = hz_to_mel(0.0), mmax = hz_to_mel(8000.0);
+    for (int i = 0; i < n_mels + 2; ++i) mel_f[i] = mel_to_hz(mmin + (mmax - mmin) * i / (n_mels + 1));
+    std::vector<int> lo(n_mels), cnt(n_mels), off(n_mels);
+    std::vector<float> wts;
+    for (int m = 0; m < n_mels; ++m) {
+        const double enorm = 2.0 / (mel_f[m + 2] - mel_f[m]);
+        int first = -1, last = -1;
+        std::vector<float> row(201);
+        for (int k = 0; k < 201; ++k) {
+            const double f = k * 16000.0 / 400.0;
+            const double lower = -(mel_f[m] - f) / (mel_f[m + 1] - mel_f[m]);
+            const double upper = (mel_f[m + 2] - f) / (mel_f[m + 2] - mel_f[m + 1]);
+            const double v = std::max(0.0, std::min(lower, upper)) * enorm;
+            row[k] = (float)v;
+            if (v > 0) {
+                if (first < 0) first = k;
+                last = k;
+            }
+        }
+        if (first < 0) first = last = 0;
+        lo[m] = first;
+        cnt[m] = last - first + 1;
+        off[m] = (int)wts.size();
+        for (int k = first; k <= last; ++k) wts.push_back(row[k]);
+    }
+    c->tw400 = dalloc<float2>(400, c->owned);
+    c->hann = dalloc<float>(400, c->owned);
+    c->flo = dalloc<int>(n_mels, c->owned);
+    c->fcnt = dalloc<int>(n_mels, c->owned);
+    c->foff = dalloc<int>(n_mels, c->owned);
+    c->fw = dalloc<float>(wts.size(), c->owned);
+    HIPCHK(hipMemcpy(c->tw400, tw.data(), 400 * sizeof(float2), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->hann, hn.data(), 400 * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->flo, lo.data(), n_mels * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->fcnt, cnt.data(), n_mels * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->foff, off.data(), n_mels * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->fw, wts.data(), wts.size() * 4, hipMemcpyHostToDevice));
+}
+
+void setup_workspace(osw_ctx* c) {
+    const osw_dims& d = c->d;
+    const int64_t B = c->B, De = d.n_audio_state, Dd = d.n_text_state;
+    const int64_t Me = B * T_ENC;
+    auto& o = c->owned;
+    c->win = dalloc<int>(3 * B, o);
+    c->X1 = dalloc<h16>(B * 3002 * c->C1, o);
+    c->H1 = dalloc<h16>(B * 3001 * De, o);
+    HIPCHK(hipMemset(c->H1, 0, (size_t)B * 3001 * De * 2));  // row 0 of every window stays zero
+    c->X = dalloc<float>(Me * De, o);
+    c->Xn = dalloc<h16>(Me * De, o);
+    c->QKV = dalloc<h16>(3 * Me * De, o);
+    c->O = dalloc<h16>(Me * De, o);
+    c->Hf = dalloc<h16>(Me * 4 * De, o);
+    c->E = dalloc<h16>(Me * De, o);
+    c->XKV = dalloc<h16>((int64_t)d.n_text_layer * 2 * Me * Dd, o);
+    c->xd = dalloc<float>(B * Dd, o);
+    c->xdn = dalloc<h16>(B * Dd, o);
+    c->dqkv = dalloc<h16>(B * 3 * Dd, o);
+    c->dattn = dalloc<h16>(B * Dd, o);
+    c->dq = dalloc<h16>(B * Dd, o);
+    c->dh = dalloc<h16>(B * 4 * Dd, o);
+    const int64_t kvn = (int64_t)d.n_text_layer * B * d.n_text_ctx * Dd;
+    c->kc = dalloc<h16>(kvn, o);
+    c->vc = dalloc<h16>(kvn, o);
+    c->logits = dalloc<float>(B * d.n_vocab, o);
+    c->cur_tok = dalloc<int>(B, o);
+    c->pos = dalloc<int>(1, o);
+    c->tokens = dalloc<int>(B * d.n_text_ctx, o);
+    c->prompt = dalloc<int>(B * d.n_text_ctx, o);
+    c->done = dalloc<int>(1, o);
+    c->supmask = dalloc<unsigned>((d.n_vocab + 31) / 32, o);
+    c->sel = dalloc<char>((size_t)B * sel_state_bytes(), o);
+    {
+        const int64_t Bm = std::min<int64_t>(B, 64);
+        const int64_t shapes[][2] = {{3 * Dd, Dd}, {Dd, Dd}, {4 * Dd, Dd}, {Dd, 4 * Dd}, {d.n_vocab, Dd}};
+        for (auto& nk : shapes)
+            c->part_floats = std::max<int64_t>(c->part_floats, skinny_ksplit((int)nk[0], (int)nk[1]) * Bm * nk[0]);
+        c->part = dalloc<float>(c->part_floats, o);
+    }
+    HIPCHK(hipHostMalloc((void**)&c->done_host, sizeof(int), 0));
+}
+
+// ------------------------------ GEMM helper ---------------------------------
+GemmArgs gemm_plain(const h16* A, int64_t lda, const h16* Wt, const float* bias, int M, int N, int K, void* C,
+                    int64_t ldc, int epi) {
+    GemmArgs g{};
+    g.A = A; g.lda = lda; g.a_grp_rows = M; g.a_grp_stride = 0;
+    g.W = Wt; g.ldw = K; g.bias = bias; g.M = M; g.N = N; g.K = K;
+    g.C = C; g.ldc = ldc; g.c_grp_rows = M; g.c_grp_stride = 0; g.pos = nullptr; g.epi = epi;
+    return g;
+}
+
+bool skinny_ok(const GemmArgs& g) {
+    return g.M <= 64 && g.K % 128 == 0 &&
+           (g.epi == EPI_F16 || g.epi == EPI_F16_GELU || g.epi == EPI_F32_RESID || g.epi == EPI_F32);
+}
+
+void run_gemm(osw_ctx* c, const GemmArgs& g, int cls) {
+    REQUIRE(g.K % 64 == 0, "GEMM K must be a multiple of 64");
+    Timed t(c, cls, 2.0 * g.M * g.N * g.K);
+    if (skinny_ok(g)) {
+        REQUIRE((int64_t)skinny_ksplit(g.N, g.K) * g.M * g.N <= c->part_floats, "split-K workspace too small");
+        launch_gemm_skinny(g, c->part, c->stream);
+    } else {
+        launch_gemm(g, c->stream);
+    }
+    HIPCHK(hipGetLastError());
+}
+
+// ---------------------------- encoder --------------------------------------
+void encoder_layer(osw_ctx* c, int i, int nb) {
+    const osw_dims& d = c->d;
+    const int De = d.n_audio_state, H = d.n_audio_head;
+    const int M = nb * T_ENC;
+    const std::string p = "enc.l" + std::to_string(i);
+    launch_layernorm(c->X, M, De, WF(c, p + ".ln1.g"), WF(c, p + ".ln1.b"), c->Xn, c->stream);
+    GemmArgs g = gemm_plain(c->Xn, De, WH(c, p + ".qkv.w"), WF(c, p + ".qkv.b"), M, 3 * De, De, c->QKV, 0, EPI_HEADS);
+    g.heads_T = T_ENC; g.heads_H = H; g.heads_nb = nb;
+    run_gemm(c, g, CL_ENC_GEMM);
+    {
+        Timed t(c, CL_ENC_ATTN, 4.0 * nb * H * (double)T_ENC * T_ENC * 64);
+        launch_enc_attn(c->QKV, c->O, T_ENC, H, nb, c->stream);
+        HIPCHK(hipGetLastError());
+    }
+    run_gemm(c, gemm_plain(c->O, De, WH(c, p + ".o.w"), WF(c, p + ".o.b"), M, De, De, c->X, De, EPI_F32_RESID),
+             CL_ENC_GEMM);
+    launch_layernorm(c->X, M, De, WF(c, p + ".ln2.g"), WF(c, p + ".ln2.b"), c->Xn, c->stream);
+    run_gemm(c, gemm_plain(c->Xn, De, WH(c, p + ".fc1.w"), WF(c, p + ".fc1.b"), M, 4 * De, De, c->Hf, 4 * De,
+                           EPI_F16_GELU), CL_ENC_GEMM);
+    run_gemm(c, gemm_plain(c->Hf, 4 * De, WH(c, p + ".fc2.w"), WF(c, p + ".fc2.b"), M, De, 4 * De, c->X, De,
+                           EPI_F32_RESID), CL_ENC_GEMM);
+}
+
+void encode(osw_ctx* c, const osw_window* wins, int n) {
+    REQUIRE(c->finalized, "weights not finalized");
+    REQUIRE(n >= 1 && n <= c->B, "window count out of range");
+    const osw_dims& d = c->d;
+    const int De = d.n_audio_state;
+    std::vector<int> hw(3 * n);
+    for (int i = 0; i < n; ++i) {
+        REQUIRE(wins[i].clip >= 0 && wins[i].clip < c->n_clips, "window clip out of range");
+        REQUIRE(wins[i].seek >= 0 && wins[i].seek < c->nframes[wins[i].clip], "window seek out of range");
+        REQUIRE(wins[i].segment_size >= 1, "empty window");
+        hw[i] = wins[i].clip;
+        hw[n + i] = wins[i].seek;
+        hw[2 * n + i] = std::min(wins[i].segment_size, N_FR);
+    }
+    HIPCHK(hipMemcpyAsync(c->win, hw.data(), hw.size() * 4, hipMemcpyHostToDevice, c->stream));
+    {
+        Timed t(c, CL_STAGE_ENC, 0);
+        launch_mel_window(c->logmel, c->mel_off_d, c->nframes_d, c->clip_max, c->win, c->win + n, c->win + 2 * n, n,
+                          d.n_mels, c->C1, c->X1, c->stream);
+        // conv1: A row (w, t) = X1[w][t .. t+2][:] (3 rows of C1) ; C row -> H1[w][1 + t]
+        GemmArgs g{};
+        g.A = c->X1; g.lda = c->C1; g.a_grp_rows = N_FR; g.a_grp_stride = 3002LL * c->C1;
+        g.W = WH(c, "enc.conv1.w"); g.ldw = 3 * c->C1; g.bias = WF(c, "enc.conv1.b");
+        g.M = n * N_FR; g.N = De; g.K = 3 * c->C1;
+        g.C = c->H1 + De; g.ldc = De; g.c_grp_rows = N_FR; g.c_grp_stride = 3001LL * De; g.epi = EPI_F16_GELU;
+        run_gemm(c, g, CL_ENC_GEMM);
+        // conv2 (stride 2): A row (w, t) = H1[w][2t .. 2t+2][:]  (H1 row r = input frame r-1)
+        GemmArgs g2{};
+        g2.A = c->H1; g2.lda = 2LL * De; g2.a_grp_rows = T_ENC; g2.a_grp_stride = 3001LL * De;
+        g2.W = WH(c, "enc.conv2.w"); g2.ldw = 3LL * De; g2.bias = WF(c, "enc.conv2.b");
+        g2.M = n * T_ENC; g2.N = De; g2.K = 3 * De;
+        g2.C = c->X; g2.ldc = De; g2.c_grp_rows = T_ENC; g2.c_grp_stride = (int64_t)T_ENC * De;
+        g2.pos = WF(c, "enc.pos"); g2.epi = EPI_F32_GELU_POS;
+        run_gemm(c, g2, CL_ENC_GEMM);
+        for (int i = 0; i < d.n_audio_layer; ++i) encoder_layer(c, i, n);
+        launch_layernorm(c->X, (int64_t)n * T_ENC, De, WF(c, "enc.lnpost.g"), WF(c, "enc.lnpost.b"), c->E, c->stream);
+    }
+    {
+        Timed t(c, CL_STAGE_XKV, 0);
+        GemmArgs g = gemm_plain(c->E, De, WH(c, "dec.crosskv.w"), WF(c, "dec.crosskv.b"), n * T_ENC,
+                                d.n_text_layer * 2 * d.n_text_state, De, c->XKV, 0, EPI_HEADS);
+        g.heads_T = T_ENC; g.heads_H = d.n_text_head; g.heads_nb = n;
+        run_gemm(c, g, 0);
+    }
+    HIPCHK(hipGetLastError());
+    c->n_encoded = n;
+}
+
+// ---------------------------- decoder --------------------------------------
+void decoder_step(osw_ctx* c, int nb) {
+    const osw_dims& d = c->d;
+    const int D = d.n_text_state, H = d.n_text_head, L = d.n_text_layer;
+    const int64_t xkv_which = (int64_t)nb * H * T_ENC * 64;
+    const int64_t kv_layer = (int64_t)nb * H * d.n_text_ctx * 64;
+    launch_dec_embed(WH(c, "dec.tok"), WF(c, "dec.pos"), c->cur_tok, c->pos, nb, D, d.n_text_ctx, c->xd, c->stream);
+    for (int l = 0; l < L; ++l) {
+        const std::string p = "dec.l" + std::to_string(l);
+        launch_layernorm(c->xd, nb, D, WF(c, p + ".ln1.g"), WF(c, p + ".ln1.b"), c->xdn, c->stream);
+        run_gemm(c, gemm_plain(c->xdn, D, WH(c, p + ".qkv.w"), WF(c, p + ".qkv.b"), nb, 3 * D, D, c->dqkv, 3 * D,
+                               EPI_F16), 0);
+        launch_dec_self_attn(c->dqkv, c->kc + l * kv_layer, c->vc + l * kv_layer, c->pos, nb, H, d.n_text_ctx,
+                             c->dattn, c->stream);
+        run_gemm(c, gemm_plain(c->dattn, D, WH(c, p + ".o.w"), WF(c, p + ".o.b"), nb, D, D, c->xd, D, EPI_F32_RESID),
+                 0);
+        launch_layernorm(c->xd, nb, D, WF(c, p + ".ln2.g"), WF(c, p + ".ln2.b"), c->xdn, c->stream);
+        run_gemm(c, gemm_plain(c->xdn, D, WH(c, p + ".xq.w"), WF(c, p + ".xq.b"), nb, D, D, c->dq, D, EPI_F16), 0);
+        {
+            Timed t(c, CL_XATTN, 2.0 * nb * H * (double)T_ENC * 64 * 2);
+            launch_dec_cross_attn(c->dq, c->XKV + (2 * l) * xkv_which, c->XKV + (2 * l + 1) * xkv_which, nb, H, T_ENC,
+                                  c->dattn, c->stream);
+        }
+        run_gemm(c, gemm_plain(c->dattn, D, WH(c, p + ".xo.w"), WF(c, p + ".xo.b"), nb, D, D, c->xd, D,
+                               EPI_F32_RESID), 0);
+        launch_layernorm(c->xd, nb, D, WF(c, p + ".ln3.g"), WF(c, p + ".ln3.b"), c->xdn, c->stream);
+        run_gemm(c, gemm_plain(c->xdn, D, WH(c, p + ".fc1.w"), WF(c, p + ".fc1.b"), nb, 4 * D, D, c->dh, 4 * D,
+                               EPI_F16_GELU), 0);
+        run_gemm(c, gemm_plain(c->dh, 4 * D, WH(c, p + ".fc2.w"), WF(c, p + ".fc2.b"), nb, D, 4 * D, c->xd, D,
+                               EPI_F32_RESID), 0);
+    }
+    launch_layernorm(c->xd, nb, D, WF(c, "dec.lnpost.g"), WF(c, "dec.lnpost.b"), c->xdn, c->stream);
+    run_gemm(c, gemm_plain(c->xdn, D, WH(c, "dec.tok"), nullptr, nb, d.n_vocab, D, c->logits, d.n_vocab, EPI_F32), 0);
+}
+
+void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) {
+    REQUIRE(nb >= 1 && nb == c->n_encoded, "decode window count must equal the last encode call");
+    REQUIRE(o && r && r->tokens && r->n_tokens && r->sum_logprob && r->no_speech_prob && r->language,
+            "null decode argument");
+    const osw_dims& d = c->d;
+    const int V = d.n_vocab;
+    const int n_pre = o->n_prefix;
+    REQUIRE(n_pre >= 0 && (n_pre == 0 || o->prefix_tokens), "bad prefix");
+    const int P = n_pre + 3 + (o->without_timestamps ? 1 : 0);
+    const int max_len = std::min(o->max_length > 0 ? o->max_length : d.n_text_ctx, d.n_text_ctx);
+    REQUIRE(P < max_len, "prompt longer than max_length");
+    std::vector<int> prompt((size_t)nb * P);
+    for (int b = 0; b < nb; ++b) {
+        int* pr = &prompt[(size_t)b * P];
+        for (int i = 0; i < n_pre; ++i) pr[i] = o->prefix_tokens[(size_t)b * n_pre + i];
+        pr[n_pre] = o->sot;
+        pr[n_pre + 1] = o->language_token;  // -1: detect
+        pr[n_pre + 2] = o->task_token;
+        if (o->without_timestamps) pr[n_pre + 3] = o->no_timestamps;
+    }
+    std::vector<unsigned> mask((V + 31) / 32, 0u);
+    for (int i = 0; i < o->n_suppress; ++i) {
+        const int t = o->suppress_tokens[i];
+        if (t >= 0 && t < V) mask[t >> 5] |= 1u << (t & 31);
+    }
+    std::vector<int> first(nb);
+    for (int b = 0; b < nb; ++b) first[b] = prompt[(size_t)b * P];
+    HIPCHK(hipMemcpyAsync(c->prompt, prompt.data(), prompt.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->supmask, mask.data(), mask.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->cur_tok, first.data(), nb * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemsetAsync(c->pos, 0, 4, c->stream));
+    HIPCHK(hipMemsetAsync(c->sel, 0, (size_t)nb * sel_state_bytes(), c->stream));
+    const int max_tok = std::max(1, max_len - P);
+    auto one_step = [&] {
+        decoder_step(c, nb);
+        launch_select(c->logits, nb, c->pos, P, n_pre, n_pre + 1, max_len, V, o->eot, o->no_speech,
+                      o->no_timestamps, o->timestamp_begin, o->blank, o->first_lang, o->n_langs, o->suppress_blank,
+                      o->without_timestamps ? 0 : 1, o->max_initial_timestamp_index, c->prompt, c->supmask, c->sel,
+                      c->cur_tok, c->tokens, max_tok, c->stream);
+        launch_bump(c->pos, c->stream);
+    };
+    const int CH = 8;
+    const bool graph = c->use_graph && !r->logits_dump;
+    if (graph) {
+        std::vector<int64_t> key = {nb, P, n_pre, max_len, o->eot, o->no_speech, o->no_timestamps,
+                                    o->timestamp_begin, o->blank, o->first_lang, o->n_langs, o->suppress_blank,
+                                    o->without_timestamps, o->max_initial_timestamp_index};
+        if (!c->dgraph || key != c->dgraph_key) {
+            if (c->dgraph) {
+                HIPCHK(hipGraphExecDestroy(c->dgraph));
+                c->dgraph = nullptr;
+            }
+            HIPCHK(hipStreamSynchronize(c->stream));
+            hipGraph_t gr = nullptr;
+            c->capturing = true;
+            try {
+                HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+                for (int i = 0; i < CH; ++i) one_step();
+                HIPCHK(hipStreamEndCapture(c->stream, &gr));
+            } catch (...) {
+                c->capturing = false;
+                hipGraph_t junk = nullptr;
+                (void)hipStreamEndCapture(c->stream, &junk);
+                if (junk) (void)hipGraphDestroy(junk);
+                throw;
+            }
+            c->capturing = false;
+            hipError_t e = hipGraphInstantiate(&c->dgraph, gr, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(gr);
+            HIPCHK(e);
+            c->dgraph_key = key;
+        }
+    }
+    int steps = 0;
+    {
+        Timed t(c, CL_STAGE_DEC, 0);
+        int since_check = 0;
+        while (steps < max_len) {
+            int did;
+            if (graph && max_len - steps >= CH) {
+                HIPCHK(hipGraphLaunch(c->dgraph, c->stream));
+                did = CH;
+            } else {
+                const int samp = steps - (P - 1);
+                if (r->logits_dump && samp >= 0 && samp < r->dump_steps) {
+                    decoder_step(c, nb);
+                    for (int b = 0; b < nb; ++b)
+                        HIPCHK(hipMemcpyAsync(r->logits_dump + ((size_t)b * r->dump_steps + samp) * V,
+                                              c->logits + (size_t)b * V, (size_t)V * 4, hipMemcpyDeviceToHost,
+                                              c->stream));
+                    launch_select(c->logits, nb, c->pos, P, n_pre, n_pre + 1, max_len, V, o->eot, o->no_speech,
+                                  o->no_timestamps, o->timestamp_begin, o->blank, o->first_lang, o->n_langs,
+                                  o->suppress_blank, o->without_timestamps ? 0 : 1, o->max_initial_timestamp_index,
+                                  c->prompt, c->supmask, c->sel, c->cur_tok, c->tokens, max_tok, c->stream);
+                    launch_bump(c->pos, c->stream);
+                } else {
+                    one_step();
+                }
+                did = 1;
+            }
+            HIPCHK(hipGetLastError());
+            steps += did;
+            since_check += did;
+            if (steps >= P && (since_check >= CH || steps >= max_len)) {
+                since_check = 0;
+                launch_count_done(c->sel, nb, c->done, c->stream);
+                HIPCHK(hipMemcpyAsync(c->done_host, c->done, 4, hipMemcpyDeviceToHost, c->stream));
+                HIPCHK(hipStreamSynchronize(c->stream));
+                if (*c->done_host >= nb) break;
+            }
+        }
+    }
+    c->pf.decode_steps = steps;
+    // read back
+    std::vector<char> st((size_t)nb * sel_state_bytes());
+    std::vector<int> toks((size_t)nb * max_tok);
+    HIPCHK(hipMemcpyAsync(st.data(), c->sel, st.size(), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(toks.data(), c->tokens, toks.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    struct S { int n_sampled, last, penult, last_ts, done, lang; float sum_lp, nsp; };
+    static_assert(sizeof(S) == 32, "SelState layout");
+    for (int b = 0; b < nb; ++b) {
+        const S* sp = (const S*)&st[(size_t)b * sizeof(S)];
+        const int n = std::min(sp->n_sampled, std::min(max_tok, r->max_tokens));
+        r->n_tokens[b] = n;
+        for (int i = 0; i < n; ++i) r->tokens[(size_t)b * r->max_tokens + i] = toks[(size_t)b * max_tok + i];
+        r->sum_logprob[b] = sp->sum_lp;
+        r->no_speech_prob[b] = sp->nsp;
+        r->language[b] = sp->lang;
+    }
+}
+
+// ------------------------------ mel ----------------------------------------
+void log_mel(osw_ctx* c, const int16_t* pcm, const int64_t* offsets, int n, int on_device, int* nf_out) {
+    REQUIRE(n >= 1, "need at least one clip");
+    REQUIRE(pcm && offsets, "null pcm/offsets");
+    const int n_mels = c->d.n_mels;
+    const int64_t total = offsets[n] - offsets[0];
+    REQUIRE(total >= 0, "bad offsets");
+    std::vector<int64_t> offs(n + 1);
+    for (int i = 0; i <= n; ++i) {
+        offs[i] = offsets[i] - offsets[0];
+        if (i) REQUIRE(offs[i] >= offs[i - 1], "offsets must be non-decreasing");
+    }
+    if (n > c->clips_cap) {
+        const int cap = std::max(n, 2 * c->clips_cap);
+        c->offsets = dalloc<int64_t>(cap + 1, c->owned);
+        c->mel_off_d = dalloc<int64_t>(cap + 1, c->owned);
+        c->nframes_d = dalloc<int>(cap, c->owned);
+        c->clip_max = dalloc<int>(cap, c->owned);
+        c->clips_cap = cap;
+    }
+    c->nframes.assign(n, 0);
+    c->mel_off.assign(n + 1, 0);
+    int max_nf = 0;
+    for (int i = 0; i < n; ++i) {
+        const int64_t N = offs[i + 1] - offs[i];
+        c->nframes[i] = (int)((N + 160) / 160);
+        c->mel_off[i + 1] = c->mel_off[i] + (int64_t)c->nframes[i] * n_mels;
+        max_nf = std::max(max_nf, c->nframes[i]);
+    }
+    if ((size_t)c->mel_off[n] > c->logmel_cap) {
+        c->logmel_cap = (size_t)c->mel_off[n] + (size_t)c->mel_off[n] / 2;
+        c->logmel = dalloc<float>(c->logmel_cap, c->owned);
+    }
+    const int16_t* src = pcm + offsets[0];
+    if (!on_device) {
+        if ((size_t)total > c->pcm_cap) {
+            c->pcm_cap = (size_t)total + (size_t)total / 2 + 1;
+            c->pcm = dalloc<int16_t>(c->pcm_cap, c->owned);
+        }
+        if (total) HIPCHK(hipMemcpyAsync(c->pcm, src, (size_t)total * 2, hipMemcpyHostToDevice, c->stream));
+        src = c->pcm;
+    }
+    HIPCHK(hipMemcpyAsync(c->offsets, offs.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->mel_off_d, c->mel_off.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->nframes_d, c->nframes.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+    {
+        Timed t(c, CL_STAGE_MEL, 0);
+        Timed k(c, CL_MEL, (double)total * 2 + (double)c->mel_off[n] * 4);
+        launch_mel(src, c->offsets, c->mel_off_d, c->nframes_d, n, max_nf, c->tw400, c->hann, c->flo, c->fcnt,
+                   c->foff, c->fw, n_mels, c->logmel, c->clip_max, c->stream);
+        HIPCHK(hipGetLastError());
+    }
+    c->n_clips = n;
+    if (nf_out)
+        for (int i = 0; i < n; ++i) nf_out[i] = c->nframes[i];
+}
+
+}  // namespace
+
+// ============================== C ABI =======================================
+extern "C" {
+
+const char* osw_version(void) { return "osw-hip 0.1 gfx950"; }
+const char* osw_last_error(void) { return g_err.c_str(); }
+
+int osw_device_count(int32_t* out) {
+    return guard([&] {
+        int n = 0;
+        HIPCHK(hipGetDeviceCount(&n));
+        *out = n;
+    });
+}
+
+int osw_create(const osw_dims* dims, int32_t device, int32_t max_batch, osw_ctx** out) {
+    osw_ctx* c = nullptr;
+    int rc = guard([&] {
+        REQUIRE(dims && out, "null argument");
+        REQUIRE(max_batch >= 1 && max_batch <= 1024, "max_batch out of range");
+        REQUIRE(dims->n_audio_state % 128 == 0 && dims->n_text_state % 128 == 0, "model width must be a multiple of 128");
+        REQUIRE(dims->n_audio_state / dims->n_audio_head == 64 && dims->n_text_state / dims->n_text_head == 64,
+                "head_dim must be 64");
+        REQUIRE(dims->n_audio_ctx == T_ENC, "n_audio_ctx must be 1500");
+        REQUIRE(dims->n_text_ctx <= 448, "n_text_ctx must be <= 448");
+        REQUIRE(dims->n_audio_state == dims->n_text_state, "encoder and decoder width must match");
+        REQUIRE(dims->n_audio_state <= 1280, "model width > 1280 unsupported");
+        int ndev = 0;
+        HIPCHK(hipGetDeviceCount(&ndev));
+        REQUIRE(device >= 0 && device < ndev, "device ordinal out of range");
+        c = new osw_ctx();
+        c->device = device;
+        c->d = *dims;
+        c->B = max_batch;
+        c->C1 = (dims->n_mels + 63) / 64 * 64;
+        if (const char* e = std::getenv("OSW_NO_GRAPH")) c->use_graph = !(e[0] == '1');
+        HIPCHK(hipSetDevice(device));
+        HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        build_weight_table(c);
+        setup_mel(c);
+        setup_workspace(c);
+        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipDeviceSynchronize());
+        *out = c;
+    });
+    if (rc != OSW_OK && c) {
+        for (void* p : c->owned) (void)hipFree(p);
+        if (c->stream) (void)hipStreamDestroy(c->stream);
+        delete c;
+    }
+    return rc;
+}
+
+int osw_destroy(osw_ctx* c) {
+    if (!c) return OSW_OK;
+    return guard([&] {
+        {
+            std::lock_guard<std::mutex> lk(c->mu);
+            HIPCHK(hipSetDevice(c->device));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            for (auto& e : c->evs) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
+            for (auto e : c->ev_free) (void)hipEventDestroy(e);
+            if (c->dgraph) (void)hipGraphExecDestroy(c->dgraph);
+            for (void* p : c->owned) (void)hipFree(p);
+            if (c->done_host) (void)hipHostFree(c->done_host);
+            (void)hipStreamDestroy(c->stream);
+        }
+        delete c;
+    });
+}
+
+int osw_set_weight(osw_ctx* c, const char* name, const void* host, int64_t nbytes) {
+    return guard([&] {
+        REQUIRE(c && name && host, "null argument");
+        std::lock_guard<std::mutex> lk(c->mu);
+        HIPCHK(hipSetDevice(c->device));
+        Tensor& t = W(c, name);
+        const std::string nm(name);
+        if (nm == "enc.conv1.w" && c->C1 != c->d.n_mels) {
+            const int64_t De = c->d.n_audio_state, M = c->d.n_mels;
+            REQUIRE(nbytes == De * 3 * M * 2, "enc.conv1.w: wrong byte count");
+            std::vector<uint16_t> pad((size_t)De * 3 * c->C1, 0);
+            const uint16_t* src = (const uint16_t*)host;
+            for (int64_t o = 0; o < De; ++o)
+                for (int k = 0; k < 3; ++k)
+                    std::memcpy(&pad[(o * 3 + k) * c->C1], &src[(o * 3 + k) * M], M * 2);
+            HIPCHK(hipMemcpy(t.ptr, pad.data(), pad.size() * 2, hipMemcpyHostToDevice));
+        } else {
+            REQUIRE(nbytes == t.numel * (t.f16 ? 2 : 4), "tensor " + nm + ": wrong byte count");
+            HIPCHK(hipMemcpy(t.ptr, host, nbytes, hipMemcpyHostToDevice));
+        }
+        t.set = true;
+    });
+}
+
+int osw_init_weight_uniform(osw_ctx* c, const char* name, uint64_t seed, int64_t stream, float scale, float offset,
+                            int64_t zero_lo, int64_t zero_hi) {
+    return guard([&] {
+        REQUIRE(c && name, "null argument");
+        std::lock_guard<std::mutex> lk(c->mu);
+        HIPCHK(hipSetDevice(c->device));
+        Tensor& t = W(c, name);
+        REQUIRE(!(std::string(name) == "enc.conv1.w" && c->C1 != c->d.n_mels),
+                "enc.conv1.w needs osw_set_weight when n_mels is not a multiple of 64");
+        launch_init_uniform(t.ptr, t.f16, t.numel, hash_stream_key(seed, stream), scale, offset, zero_lo, zero_hi,
+                            c->stream);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(c->stream));
+        t.set = true;
+    });
+}
+
+int osw_finalize(osw_ctx* c) {
+    return guard([&] {
+        REQUIRE(c, "null ctx");
+        std::lock_guard<std::mutex> lk(c->mu);
+        std::string missing;
+        for (auto& kv : c->w)
+            if (!kv.second.set) missing += kv.first + " ";
+        REQUIRE(missing.empty(), "missing tensors: " + missing);
+        c->finalized = true;
+    });
+}
+
+int osw_log_mel(osw_ctx* c, const int16_t* pcm, const int64_t* offsets, int32_t n_clips, int32_t pcm_on_device,
+                int32_t* n_frames) {
+    return guard([&] {
+        REQUIRE(c, "null ctx");
+        std::lock_guard<std::mutex> lk(c->mu);
+        HIPCHK(hipSetDevice(c->device));
+        log_mel(c, pcm, offsets, n_clips, pcm_on_device, n_frames);
+        HIPCHK(hipStreamSynchronize(c->stream));
+        resolve_events(c);
+    });
+}
+
+int osw_get_mel(osw_ctx* c, int32_t clip, float* out, int64_t out_floats) {
+    return guard([&] {
+        REQUIRE(c && out, "null argument");
+        std::lock_guard<std::mutex> lk(c->mu);
+        HIPCHK(hipSetDevice(c->device));
+        REQUIRE(clip >= 0 && clip < c->n_clips, "clip out of range");
+        const int nf = c->nframes[clip];
+        const int64_t n = (int64_t)nf * c->d.n_mels;
+        REQUIRE(out_floats >= n, "output buffer too small");
+        float* tmp = nullptr;
+        HIPCHK(hipMalloc(&tmp, n * 4));
+        launch_mel_normalize(c->logmel, c->mel_off[clip], nf, c->d.n_mels, c->clip_max, clip, tmp, c->stream);
+        hipError_t e = hipMemcpyAsync(out, tmp, n * 4, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        (void)hipFree(tmp);
+        HIPCHK(e);
+    });
+}
+
+int osw_encode_windows(osw_ctx* c, const osw_window* windows, int32_t n) {
+    return guard([&] {
+        REQUIRE(c && windows, "null argument");
+        std::lock_guard<std::mutex> lk(c->mu);
+        HIPCHK(hipSetDevice(c->device));
+        encode(c, windows, n);
+        HIPCHK(hipStreamSynchronize(c->stream));
+        resolve_events(c);
+    });
+}
+
+int osw_get_encoder_output(osw_ctx* c, int32_t window, float* out, int64_t out_floats) {
+    return guard([&] {
+        REQUIRE(c && out, "null argument");
+        std::lock_guard<std::mutex> lk(c->mu);
+        HIPCHK(hipSetDevice(c->device));
+        REQUIRE(window >= 0 && window < c->n_encoded, "window out of range");
+        const int64_t n = (int64_t)T_ENC * c->d.n_audio_state;
+        REQUIRE(out_floats >= n, "output buffer too small");
+        std::vector<_Float16> tmp(n);
+        HIPCHK(hipMemcpy(tmp.data(), c->E + window * n, n * 2, hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < n; ++i) out[i] = (float)tmp[i];
+    });
+}
+
+int osw_decode_windows(osw_ctx* c, int32_t n, const osw_decode_opts* opts, osw_window_result* res) {
+    return guard([&] {
+        REQUIRE(c, "null ctx");
+        std::lock_guard<std::mutex> lk(c->mu);
+        HIPCHK(hipSetDevice(c->device));
+        decode(c, n, opts, res);
+        resolve_events(c);
+    });
+}
+
+int osw_transcribe_batch(osw_ctx* c, const int16_t* pcm, const int64_t* offsets, int32_t n_clips,
+                         int32_t pcm_on_device, const osw_decode_opts* opts, osw_window_result* res) {
+    return guard([&] {
+        REQUIRE(c, "null ctx");
+        std::lock_guard<std::mutex> lk(c->mu);
+        HIPCHK(hipSetDevice(c->device));
+        REQUIRE(n_clips >= 1 && n_clips <= c->B, "n_clips out of range");
+        log_mel(c, pcm, offsets, n_clips, pcm_on_device, nullptr);
+        std::vector<osw_window> wins(n_clips);
+        for (int i = 0; i < n_clips; ++i)
+            wins[i] = osw_window{i, 0, std::max(1, std::min(N_FR, c->nframes[i] - 1))};
+        encode(c, wins.data(), n_clips);
+        decode(c, n_clips, opts, res);
+        resolve_events(c);
+    });
+}
+
+int osw_encoder_layer_debug(osw_ctx* c, int32_t layer, const float* x, float* y, int32_t T) {
+    return guard([&] {
+        REQUIRE(c && x && y, "null argument");
+        std::lock_guard<std::mutex> lk(c->mu);
+        HIPCHK(hipSetDevice(c->device));
+        REQUIRE(c->finalized, "weights not finalized");
+        REQUIRE(T == T_ENC, "T must be 1500");
+        REQUIRE(layer >= 0 && layer < c->d.n_audio_layer, "layer out of range");
+        const int64_t n = (int64_t)T * c->d.n_audio_state;
+        HIPCHK(hipMemcpyAsync(c->X, x, n * 4, hipMemcpyHostToDevice, c->stream));
+        encoder_layer(c, layer, 1);
+        HIPCHK(hipMemcpyAsync(y, c->X, n * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        resolve_events(c);
+    });
+}
+
+int osw_set_profiling(osw_ctx* c, int32_t enable) {
+    return guard([&] {
+        REQUIRE(c, "null ctx");
+        std::lock_guard<std::mutex> lk(c->mu);
+        c->prof = enable != 0;
+        c->pf = osw_profile{};
+    });
+}
+
+int osw_get_profile(osw_ctx* c, osw_profile* out) {
+    return guard([&] {
+        REQUIRE(c && out, "null argument");
+        std::lock_guard<std::mutex> lk(c->mu);
+        resolve_events(c);
+        *out = c->pf;
+    });
+}
+
+void* osw_stream(osw_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+}  // extern "C"

@@ -117,28 +117,14 @@ def main():
     cfg = DecodeConfig(suppress_tokens=sup, max_length=a.max_length)
 
     n_total = B * world
-    # inputs resident in HBM: rank 0 holds every clip (int16 bytes carried as fp16 for RCCL)
-    if rank == 0:
-        allpcm = torch.from_numpy(make_clips(n_total)).to(dev)
-    shard = torch.empty((B, 480000), dtype=torch.int16, device=dev)
-    offsets = np.arange(B + 1, dtype=np.int64) * 480000
-    tok_dev = torch.empty((B, dims.n_text_ctx), dtype=torch.int32, device=dev)
+    from open_speech_amd.distributed import DataParallelTranscriber
+
+    dp = DataParallelTranscriber(eng, cfg, dist=dist, device=dev, clips_per_rank=B, ctx=dims.n_text_ctx)
+    # inputs resident in HBM before timing: rank 0 holds every clip
+    allpcm = torch.from_numpy(make_clips(n_total)).to(dev) if rank == 0 else None
 
     def step():
-        if world > 1:
-            chunks = list(allpcm.view(torch.float16).chunk(world)) if rank == 0 else None
-            dist.scatter(shard.view(torch.float16), chunks, src=0)
-        else:
-            shard.copy_(allpcm)
-        torch.cuda.synchronize(dev)
-        outs = eng.transcribe_batch(None, cfg, device_pcm=shard.data_ptr(), offsets=offsets)
-        if world > 1:
-            t = np.full((B, dims.n_text_ctx), -1, np.int32)
-            for i, o in enumerate(outs):
-                t[i, :len(o.tokens)] = o.tokens
-            tok_dev.copy_(torch.from_numpy(t))
-            gl = [torch.empty_like(tok_dev) for _ in range(world)] if rank == 0 else None
-            dist.gather(tok_dev, gl, dst=0)
+        outs, _ = dp.step(allpcm)
         return outs
 
     for _ in range(a.warmup):

@@ -70,6 +70,9 @@ typedef struct osw_decode_opts {
     /* tokens placed BEFORE <|startoftranscript|> (e.g. <|startofprev|> + previous
      * text), n_windows * n_prefix ints, same length for every window of the call */
     const int32_t* prefix_tokens; int32_t n_prefix;
+    /* optional per-window language tokens (n_windows ints; -1 = detect); NULL: use
+     * language_token for every window */
+    const int32_t* language_tokens;
 } osw_decode_opts;
 
 /* Caller-allocated outputs for n windows. */

@@ -31,7 +31,8 @@ class osw_decode_opts(C.Structure):
                 ("eot", C.c_int32), ("sot", C.c_int32), ("sot_prev", C.c_int32), ("no_speech", C.c_int32),
                 ("no_timestamps", C.c_int32), ("timestamp_begin", C.c_int32), ("blank", C.c_int32),
                 ("first_lang", C.c_int32), ("n_langs", C.c_int32),
-                ("prefix_tokens", C.POINTER(C.c_int32)), ("n_prefix", C.c_int32)]
+                ("prefix_tokens", C.POINTER(C.c_int32)), ("n_prefix", C.c_int32),
+                ("language_tokens", C.POINTER(C.c_int32))]
 
 
 class osw_window_result(C.Structure):

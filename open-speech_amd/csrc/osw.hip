@@ -558,7 +558,7 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
         int* pr = &prompt[(size_t)b * P];
         for (int i = 0; i < n_pre; ++i) pr[i] = o->prefix_tokens[(size_t)b * n_pre + i];
         pr[n_pre] = o->sot;
-        pr[n_pre + 1] = o->language_token;  // -1: detect
+        pr[n_pre + 1] = o->language_tokens ? o->language_tokens[b] : o->language_token;  // -1: detect
         pr[n_pre + 2] = o->task_token;
         if (o->without_timestamps) pr[n_pre + 3] = o->no_timestamps;
     }

@@ -1,0 +1,144 @@
+"""Dynamic batcher + per-GPU workers behind ``transcribe()``.
+
+The reference calls ``transcribe`` concurrently from the default executor (REST,
+``src/main.py:305``), a 4-thread streaming pool (``src/streaming.py:50-52``), a
+4-thread Realtime pool (``src/realtime/server.py:33-35``) and Wyoming.  Each call
+here becomes a request on a queue; one worker thread per GPU drains up to
+``max_batch`` requests (waiting at most ``max_wait_ms`` for company once the first
+arrives), runs them as one batched seek loop on its engine, and completes each
+caller's future.  Requests are routed to the worker with the shortest queue
+(multi-GPU serving: independent clips, no collective).  A worker whose GPU fails
+marks itself dead and re-queues what it held on the survivors.
+"""
+from __future__ import annotations
+
+import queue
+import threading
+import time
+from concurrent.futures import Future
+from dataclasses import dataclass
+
+import numpy as np
+
+from .segments import ClipResult, TranscribeOptions, transcribe_clips
+from .tokenizer import WhisperTokenizer, get_suppressed_tokens
+
+
+@dataclass
+class _Req:
+    pcm: np.ndarray
+    opts: TranscribeOptions
+    fut: Future
+
+
+class _Worker(threading.Thread):
+    def __init__(self, pool: "BatchRunner", engine, idx: int):
+        super().__init__(daemon=True, name=f"osw-worker-{idx}")
+        self.pool, self.engine, self.idx = pool, engine, idx
+        self.q: "queue.Queue[_Req | None]" = queue.Queue()
+        self.alive = True
+        self.inflight = 0
+
+    def load(self) -> int:
+        return self.q.qsize() + self.inflight
+
+    def run(self) -> None:
+        while True:
+            first = self.q.get()
+            if first is None:
+                return
+            batch = [first]
+            deadline = time.monotonic() + self.pool.max_wait_ms / 1000.0
+            while len(batch) < self.engine.max_batch:
+                left = deadline - time.monotonic()
+                try:
+                    nxt = self.q.get(timeout=max(0.0, left)) if left > 0 else self.q.get_nowait()
+                except queue.Empty:
+                    break
+                if nxt is None:
+                    self.q.put(None)
+                    break
+                batch.append(nxt)
+            self.inflight = len(batch)
+            try:
+                self._run_batch(batch)
+            except Exception as e:  # noqa: BLE001 - forwarded to callers
+                if self.pool.is_device_error(e) and len(self.pool.workers) > 1:
+                    self.alive = False
+                    for r in batch:
+                        self.pool.submit_req(r, exclude=self)
+                    self.pool.drain_dead(self)
+                    return
+                for r in batch:
+                    if not r.fut.done():
+                        r.fut.set_exception(e)
+            finally:
+                self.inflight = 0
+
+    def _run_batch(self, batch: list) -> None:
+        groups: dict = {}
+        for r in batch:
+            groups.setdefault(r.opts.key(), []).append(r)
+        for reqs in groups.values():
+            res = transcribe_clips(self.engine, [r.pcm for r in reqs], reqs[0].opts, self.pool.tokenizer,
+                                   self.pool.suppress_for(reqs[0].opts))
+            for r, out in zip(reqs, res):
+                r.fut.set_result(out)
+
+
+class BatchRunner:
+    def __init__(self, engines: list, tokenizer: WhisperTokenizer, max_wait_ms: float = 5.0):
+        self.tokenizer = tokenizer
+        self.max_wait_ms = max_wait_ms
+        self._sup_cache: dict = {}
+        self._lock = threading.Lock()
+        self.workers = [_Worker(self, e, i) for i, e in enumerate(engines)]
+        for w in self.workers:
+            w.start()
+
+    def suppress_for(self, opts: TranscribeOptions) -> tuple:
+        key = tuple(opts.suppress_tokens)
+        if key not in self._sup_cache:
+            self._sup_cache[key] = get_suppressed_tokens(self.tokenizer, list(opts.suppress_tokens))
+        return self._sup_cache[key]
+
+    @staticmethod
+    def is_device_error(e: Exception) -> bool:
+        s = str(e)
+        return "hipError" in s or "(-100)" in s
+
+    def submit_req(self, r: _Req, exclude=None) -> None:
+        with self._lock:
+            live = [w for w in self.workers if w.alive and w is not exclude]
+            if not live:
+                r.fut.set_exception(RuntimeError("no live GPU worker"))
+                return
+            w = min(live, key=lambda x: x.load())
+            w.q.put(r)
+
+    def drain_dead(self, dead: _Worker) -> None:
+        while True:
+            try:
+                r = dead.q.get_nowait()
+            except queue.Empty:
+                return
+            if r is not None:
+                self.submit_req(r, exclude=dead)
+
+    def submit(self, pcm: np.ndarray, opts: TranscribeOptions) -> Future:
+        f: Future = Future()
+        self.submit_req(_Req(np.ascontiguousarray(pcm, dtype=np.int16), opts, f))
+        return f
+
+    def transcribe(self, pcm: np.ndarray, opts: TranscribeOptions, timeout: float | None = None) -> ClipResult:
+        return self.submit(pcm, opts).result(timeout=timeout)
+
+    def close(self) -> None:
+        for w in self.workers:
+            w.q.put(None)
+        for w in self.workers:
+            w.join(timeout=30)
+        for w in self.workers:
+            close = getattr(w.engine, "close", None)
+            if close:
+                close()

@@ -1,0 +1,250 @@
+"""Window scheduling and segment assembly (faster-whisper 1.2.1 ``generate_segments``,
+upstream, not vendored), batched across clips.
+
+For every clip the 30 s seek loop of faster-whisper runs unchanged — window k+1
+depends on window k's last timestamp and (with ``condition_on_previous_text``) its
+tokens — but the windows of DIFFERENT clips that are due at the same time are
+encoded and decoded together on the GPU (grouped by prompt length, since every
+window of one decode call shares its prompt length).
+
+Semantics restated (greedy, single temperature 0.0 — the reference passes a scalar
+``temperature`` at ``src/backends/faster_whisper.py:238``, so there is no fallback):
+  content_frames = n_frames - 1; segment_size = min(3000, content_frames - seek)
+  prompt = [<|startofprev|>] + previous_tokens[-223:] (if any) + [sot, lang, task]
+  avg_logprob = sum_logprob / (len(tokens) + 1); compression_ratio of the window text
+  skip window if no_speech_prob > 0.6 and avg_logprob < -1.0  (seek += segment_size)
+  split at consecutive timestamp pairs; single timestamp ending -> seek += segment_size,
+  else seek += last_timestamp_position * 2; drop segments with start == end or blank text
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from .dims import INPUT_STRIDE, N_FRAMES, TIME_PRECISION
+from .engine import DecodeConfig
+from .tokenizer import WhisperTokenizer, compression_ratio
+
+FRAME_SEC = 0.01
+
+
+@dataclass
+class TranscribeOptions:
+    task: str = "transcribe"
+    language: str | None = None
+    initial_prompt: str | None = None
+    condition_on_previous_text: bool = True
+    no_speech_threshold: float | None = 0.6
+    log_prob_threshold: float | None = -1.0
+    compression_ratio_threshold: float | None = 2.4
+    suppress_blank: bool = True
+    suppress_tokens: tuple = (-1,)
+    without_timestamps: bool = False
+    max_initial_timestamp: float = 1.0
+    temperature: float = 0.0
+
+    def key(self):
+        return (self.task, self.language, self.initial_prompt, self.condition_on_previous_text,
+                self.without_timestamps, tuple(self.suppress_tokens), self.suppress_blank)
+
+
+@dataclass
+class Segment:
+    id: int
+    seek: int
+    start: float
+    end: float
+    text: str
+    tokens: list
+    temperature: float
+    avg_logprob: float
+    compression_ratio: float
+    no_speech_prob: float
+
+
+@dataclass
+class ClipResult:
+    segments: list = field(default_factory=list)
+    language: str = "en"
+    duration: float = 0.0
+
+
+def split_segments_by_timestamps(tokens: list, tb: int, time_offset: float, segment_size: int,
+                                 segment_duration: float, seek: int):
+    """faster-whisper ``_split_segments_by_timestamps`` (openai transcribe.py logic)."""
+    current = []
+    single_timestamp_ending = len(tokens) >= 2 and tokens[-2] < tb <= tokens[-1]
+    consecutive = [i for i in range(len(tokens)) if i > 0 and tokens[i] >= tb and tokens[i - 1] >= tb]
+    if consecutive:
+        slices = list(consecutive)
+        if single_timestamp_ending:
+            slices.append(len(tokens))
+        last_slice = 0
+        for cur in slices:
+            sliced = tokens[last_slice:cur]
+            start_pos = sliced[0] - tb
+            end_pos = sliced[-1] - tb
+            current.append(dict(seek=seek, start=time_offset + start_pos * TIME_PRECISION,
+                                end=time_offset + end_pos * TIME_PRECISION, tokens=sliced))
+            last_slice = cur
+        if single_timestamp_ending:
+            seek += segment_size
+        else:
+            last_ts_pos = tokens[last_slice - 1] - tb
+            seek += last_ts_pos * INPUT_STRIDE
+    else:
+        duration = segment_duration
+        ts = [t for t in tokens if t >= tb]
+        if ts and ts[-1] != tb:
+            duration = (ts[-1] - tb) * TIME_PRECISION
+        current.append(dict(seek=seek, start=time_offset, end=time_offset + duration, tokens=tokens))
+        seek += segment_size
+    return current, seek, single_timestamp_ending
+
+
+@dataclass
+class _ClipState:
+    idx: int
+    content_frames: int
+    seek: int = 0
+    all_tokens: list = field(default_factory=list)
+    prompt_reset_since: int = 0
+    lang_token: int | None = None
+    done: bool = False
+    result: ClipResult = field(default_factory=ClipResult)
+
+
+def transcribe_clips(engine, pcm_list: list, opts: TranscribeOptions, tok: WhisperTokenizer,
+                     suppress: tuple) -> list[ClipResult]:
+    """Run the seek loop for a batch of int16 clips on one engine (all share `opts`)."""
+    st = tok.special
+    nf = engine.log_mel(pcm_list)
+    lang_token = tok.language_token(opts.language) if (opts.language and opts.task == "transcribe") else None
+    init_tokens = tok.encode(" " + opts.initial_prompt.strip()) if opts.initial_prompt else []
+    states = []
+    for i, n in enumerate(nf):
+        s = _ClipState(idx=i, content_frames=max(0, n - 1), all_tokens=list(init_tokens), lang_token=lang_token)
+        s.result.duration = len(pcm_list[i]) / 16000.0
+        s.done = s.content_frames <= 0
+        states.append(s)
+    max_init = int(round(opts.max_initial_timestamp / TIME_PRECISION))
+    B = engine.max_batch
+    while True:
+        active = [s for s in states if not s.done]
+        if not active:
+            break
+        # group due windows by prompt (prefix) length and by "language known"
+        groups: dict = {}
+        for s in active:
+            prev = s.all_tokens[s.prompt_reset_since:]
+            prefix = ([st.sot_prev] + prev[-(448 // 2 - 1):]) if prev else []
+            groups.setdefault((len(prefix), s.lang_token is None), []).append((s, prefix))
+        for (_plen, _detect), members in groups.items():
+            for lo in range(0, len(members), B):
+                chunk = members[lo:lo + B]
+                wins = []
+                for s, _ in chunk:
+                    size = min(N_FRAMES, s.content_frames - s.seek)
+                    wins.append((s.idx, s.seek, size))
+                engine.encode(wins)
+                langs = None if _detect else [s.lang_token for s, _ in chunk]
+                cfg = DecodeConfig(task=opts.task, language_token=None, suppress_tokens=suppress,
+                                   suppress_blank=opts.suppress_blank, without_timestamps=opts.without_timestamps,
+                                   max_initial_timestamp_index=max_init)
+                prefixes = [p for _, p in chunk] if _plen else None
+                outs = engine.decode(len(chunk), cfg, prefix=prefixes, languages=langs)
+                for (s, _), w, out in zip(chunk, wins, outs):
+                    _consume(s, w, out, opts, tok)
+    for s in states:
+        code = tok.language_code(s.lang_token) if s.lang_token is not None else (opts.language or "en")
+        s.result.language = code
+    return [s.result for s in states]
+
+
+def _consume(s: _ClipState, win, out, opts: TranscribeOptions, tok: WhisperTokenizer) -> None:
+    st = tok.special
+    _, seek, segment_size = win
+    if s.lang_token is None:
+        s.lang_token = out.language
+    tokens = out.tokens
+    avg_logprob = out.sum_logprob / (len(tokens) + 1)
+    text = tok.decode(tokens).strip()
+    cr = compression_ratio(text)
+    if opts.no_speech_threshold is not None:
+        skip = out.no_speech_prob > opts.no_speech_threshold
+        if opts.log_prob_threshold is not None and avg_logprob > opts.log_prob_threshold:
+            skip = False
+        if skip:
+            s.seek = seek + segment_size
+            s.done = s.seek >= s.content_frames
+            return
+    time_offset = seek * FRAME_SEC
+    segs, new_seek, _ = split_segments_by_timestamps(tokens, st.timestamp_begin, time_offset, segment_size,
+                                                     segment_size * FRAME_SEC, seek)
+    for sg in segs:
+        t = sg["tokens"]
+        txt = tok.decode(t)
+        if sg["start"] == sg["end"] or not txt.strip():
+            continue
+        s.all_tokens.extend(t)
+        s.result.segments.append(Segment(id=len(s.result.segments), seek=seek, start=sg["start"], end=sg["end"],
+                                         text=txt, tokens=list(t), temperature=opts.temperature,
+                                         avg_logprob=avg_logprob, compression_ratio=cr,
+                                         no_speech_prob=out.no_speech_prob))
+    if not opts.condition_on_previous_text:
+        s.prompt_reset_since = len(s.all_tokens)
+    s.seek = new_seek
+    s.done = s.seek >= s.content_frames
+
+
+def verbose_dict(task: str, res: ClipResult) -> dict:
+    """The ``verbose_json`` shape of ``src/backends/faster_whisper.py:251-272``."""
+    full = "".join(sg.text for sg in res.segments).strip()
+    return {
+        "task": task, "language": res.language, "duration": res.duration, "text": full,
+        "segments": [{"id": i, "seek": int(sg.seek), "start": sg.start, "end": sg.end, "text": sg.text,
+                      "tokens": list(sg.tokens) if sg.tokens else [], "temperature": sg.temperature,
+                      "avg_logprob": sg.avg_logprob, "compression_ratio": sg.compression_ratio,
+                      "no_speech_prob": sg.no_speech_prob} for i, sg in enumerate(res.segments)],
+    }
+
+
+def _ts(seconds: float, sep: str) -> str:
+    h = int(seconds // 3600)
+    m = int((seconds % 3600) // 60)
+    s = int(seconds % 60)
+    ms = int((seconds % 1) * 1000)
+    return f"{h:02d}:{m:02d}:{s:02d}{sep}{ms:03d}"
+
+
+def to_srt(segments) -> str:
+    """``FasterWhisperBackend._to_srt`` (src/backends/faster_whisper.py:313-321)."""
+    return "\n".join(f"{i}\n{_ts(s.start, ',')} --> {_ts(s.end, ',')}\n{s.text.strip()}\n"
+                     for i, s in enumerate(segments, 1))
+
+
+def to_vtt(segments) -> str:
+    """``FasterWhisperBackend._to_vtt`` (src/backends/faster_whisper.py:323-330)."""
+    lines = ["WEBVTT\n"]
+    for s in segments:
+        lines.append(f"{_ts(s.start, '.')} --> {_ts(s.end, '.')}\n{s.text.strip()}\n")
+    return "\n".join(lines)
+
+
+def shape_response(task: str, res: ClipResult, response_format: str) -> dict:
+    """Return shapes by format (src/backends/faster_whisper.py:251-281)."""
+    full = "".join(sg.text for sg in res.segments).strip()
+    if response_format == "verbose_json":
+        return verbose_dict(task, res)
+    if response_format == "text":
+        return {"text": full, "raw_text": True}
+    if response_format == "srt":
+        return {"text": to_srt(res.segments), "raw_text": True}
+    if response_format == "vtt":
+        return {"text": to_vtt(res.segments), "raw_text": True}
+    return {"text": full}
+
+
+def np_int16(x) -> np.ndarray:
+    return np.ascontiguousarray(x, dtype=np.int16)

@@ -1,0 +1,304 @@
+"""Host logic of the drop-in backend (no GPU): STTBackend surface, lifecycle dicts,
+response shapes, the faster-whisper seek loop / segment split, batching under
+concurrency, and WAV ingest.  The engine is a scripted stand-in with the
+WhisperEngine interface (the same seam style as the reference's FakeSTTBackend,
+tests/test_model_manager.py:14-47)."""
+import asyncio
+import io
+import threading
+import time
+import wave
+
+import numpy as np
+import pytest
+
+from open_speech_amd import dims as D
+from open_speech_amd import synth
+from open_speech_amd.audio import decode_audio_bytes, pcm16_from_wav
+from open_speech_amd.backend import HipWhisperBackend, install
+from open_speech_amd.engine import WindowOutput
+from open_speech_amd.segments import split_segments_by_timestamps, to_srt, to_vtt
+
+ST = D.SpecialTokens.for_vocab(51866)
+TB = ST.timestamp_begin
+
+
+class FakeEngine:
+    """Scripted engine: `script(window, call_index, prefix, language) -> WindowOutput`."""
+
+    def __init__(self, dims, gpu, max_batch, script=None):
+        self.dims, self.gpu, self.max_batch = dims, gpu, max_batch
+        self.script = script or (lambda w, i, p, l: WindowOutput([TB, 1000, 1001, TB + 100], -1.0, 0.01, ST.first_lang))
+        self.calls, self.batches, self.closed = [], [], False
+        self._nf = []
+        self._wins = []
+        self.lock = threading.Lock()
+
+    def init_random(self, seed=0):
+        pass
+
+    def load_weights(self, w):
+        pass
+
+    def log_mel(self, clips):
+        self._nf = [(len(c) + 160) // 160 for c in clips]
+        return self._nf
+
+    def encode(self, wins):
+        self._wins = list(wins)
+
+    def decode(self, n, cfg, prefix=None, dump_steps=0, languages=None):
+        assert n == len(self._wins)
+        self.batches.append(n)
+        outs = []
+        for k, w in enumerate(self._wins):
+            lang = None if languages is None else languages[k]
+            self.calls.append((w, prefix[k] if prefix else [], lang, cfg.task))
+            outs.append(self.script(w, len(self.calls) - 1, prefix[k] if prefix else [], lang))
+        return outs
+
+    def close(self):
+        self.closed = True
+
+
+def make_backend(script=None, holder=None):
+    def factory(dims, gpu, mb):
+        e = FakeEngine(dims, gpu, mb, script)
+        if holder is not None:
+            holder.append(e)
+        return e
+    return HipWhisperBackend(engine_factory=factory)
+
+
+def wav(seconds=30.0, i=0):
+    return synth.to_wav_bytes(synth.chirp_clip(i, seconds))
+
+
+MID = "random:micro-test"
+
+
+# --------------------------------------------------------------------------- segment split
+def test_split_pairs_single_ending():
+    toks = [TB, 10, 11, TB + 50, TB + 50, 12, TB + 120]
+    segs, seek, single = split_segments_by_timestamps(toks, TB, 0.0, 3000, 30.0, 0)
+    assert single and seek == 3000
+    assert [(s["start"], s["end"]) for s in segs] == [(0.0, 1.0), (1.0, 2.4)]
+    assert segs[0]["tokens"] == [TB, 10, 11, TB + 50]
+
+
+def test_split_unfinished_seeks_to_last_timestamp():
+    toks = [TB, 10, TB + 40, TB + 40, 11, 12]
+    segs, seek, single = split_segments_by_timestamps(toks, TB, 5.0, 3000, 30.0, 500)
+    assert not single
+    assert len(segs) == 1 and segs[0]["start"] == 5.0 and abs(segs[0]["end"] - 5.8) < 1e-9
+    assert seek == 500 + 40 * 2
+
+
+def test_split_no_pairs_uses_last_timestamp_duration():
+    toks = [TB, 10, 11, TB + 75]
+    segs, seek, _ = split_segments_by_timestamps(toks, TB, 0.0, 2000, 20.0, 0)
+    assert len(segs) == 1 and abs(segs[0]["end"] - 1.5) < 1e-9 and seek == 2000
+    segs, seek, _ = split_segments_by_timestamps([10, 11], TB, 3.0, 1000, 10.0, 300)
+    assert segs[0]["end"] == 13.0 and seek == 1300
+
+
+def test_srt_vtt_format():
+    class S:
+        def __init__(self, a, b, t):
+            self.start, self.end, self.text = a, b, t
+    s = [S(0.0, 1.5, " hi"), S(3661.25, 3662.0, " there ")]
+    assert to_srt(s) == "1\n00:00:00,000 --> 00:00:01,500\nhi\n\n2\n01:01:01,250 --> 01:01:02,000\nthere\n"
+    assert to_vtt(s).startswith("WEBVTT\n\n00:00:00.000 --> 00:00:01.500\nhi\n")
+
+
+# --------------------------------------------------------------------------- backend surface
+def test_protocol_surface_and_lifecycle():
+    b = make_backend()
+    assert b.name == "faster-whisper"
+    for m in ("load_model", "unload_model", "loaded_models", "is_model_loaded", "transcribe", "translate",
+              "list_cached_models", "delete_cached_model", "is_model_cached"):
+        assert callable(getattr(b, m))
+    assert not b.is_model_loaded(MID)
+    b.load_model(MID)
+    t0 = b._loaded_at[MID]
+    b.load_model(MID)                      # idempotent
+    assert b._loaded_at[MID] == t0
+    assert b.is_model_loaded(MID) and MID in b._models and MID in b._last_used
+    info = b.loaded_models()[0]
+    get = (lambda k: info[k]) if isinstance(info, dict) else (lambda k: getattr(info, k))
+    assert get("model") == MID and get("backend") == "faster-whisper" and get("compute_type") == "float16"
+    assert get("device").startswith("rocm:")
+    b.unload_model(MID)
+    assert not b.is_model_loaded(MID) and MID not in b._last_used and MID not in b._loaded_at
+    b.unload_model(MID)                    # no-op
+
+
+def test_autoload_and_last_used_refresh():
+    b = make_backend()
+    r = b.transcribe(wav(2.0), MID)
+    assert b.is_model_loaded(MID)
+    lu = b._last_used[MID]
+    time.sleep(0.01)
+    b.transcribe(wav(2.0), MID)
+    assert b._last_used[MID] > lu
+    assert set(r) == {"text"}
+    b.unload_model(MID)
+
+
+@pytest.mark.parametrize("fmt", ["json", "verbose_json", "text", "srt", "vtt"])
+def test_response_shapes(fmt):
+    b = make_backend()
+    r = b.transcribe(wav(5.0), MID, response_format=fmt)
+    if fmt == "verbose_json":
+        assert set(r) == {"task", "language", "duration", "text", "segments"}
+        assert r["task"] == "transcribe" and r["language"] == "en" and abs(r["duration"] - 5.0) < 1e-6
+        seg = r["segments"][0]
+        assert set(seg) == {"id", "seek", "start", "end", "text", "tokens", "temperature", "avg_logprob",
+                            "compression_ratio", "no_speech_prob"}
+        assert seg["id"] == 0 and seg["tokens"] == [TB, 1000, 1001, TB + 100]
+        assert abs(seg["avg_logprob"] - (-1.0 / 5)) < 1e-6 and seg["end"] == 2.0
+    elif fmt in ("text", "srt", "vtt"):
+        assert r["raw_text"] is True and isinstance(r["text"], str)
+    else:
+        assert set(r) == {"text"}
+    b.unload_model(MID)
+
+
+def test_translate_detects_language_and_uses_translate_task():
+    holder = []
+    b = make_backend(holder=holder)
+    r = b.translate(wav(3.0), MID, response_format="verbose_json")
+    assert r["task"] == "translate"
+    e = holder[0]
+    assert all(c[3] == "translate" for c in e.calls)
+    assert all(c[2] is None for c in e.calls)  # language detected, never forced
+    b.unload_model(MID)
+
+
+def test_language_forwarded_for_transcribe():
+    holder = []
+    b = make_backend(holder=holder)
+    b.transcribe(wav(3.0), MID, language="de")
+    assert holder[0].calls[0][2] == ST.first_lang + 2  # "de" is the 3rd language token
+    b.unload_model(MID)
+
+
+def test_seek_loop_conditions_on_previous_text():
+    """First window ends mid-segment -> second window starts at the last timestamp,
+    with <|startofprev|> + previous tokens as prompt prefix."""
+    def script(w, i, prefix, lang):
+        clip, seek, size = w
+        if seek == 0:
+            return WindowOutput([TB, 500, 501, TB + 600, TB + 600, 502], -0.5, 0.01, ST.first_lang)
+        return WindowOutput([TB, 600, TB + 30], -0.5, 0.01, ST.first_lang)
+    holder = []
+    b = make_backend(script, holder)
+    r = b.transcribe(wav(30.0), MID, response_format="verbose_json")
+    calls = holder[0].calls
+    assert calls[0][0] == (0, 0, 3000) and calls[0][1] == []
+    assert calls[1][0] == (0, 1200, 3000 - 1200)
+    assert calls[1][1] == [ST.sot_prev, TB, 500, 501, TB + 600]
+    assert calls[1][2] == ST.first_lang      # language fixed after detection
+    assert [s["seek"] for s in r["segments"]] == [0, 1200]
+    assert abs(r["segments"][1]["start"] - 12.0) < 1e-9 and abs(r["segments"][1]["end"] - 12.6) < 1e-9
+    b.unload_model(MID)
+
+
+def test_no_speech_window_skipped():
+    b = make_backend(lambda w, i, p, l: WindowOutput([TB, 5, TB + 10], -9.0, 0.95, ST.first_lang))
+    r = b.transcribe(wav(4.0), MID, response_format="verbose_json")
+    assert r["segments"] == [] and r["text"] == ""
+    b.unload_model(MID)
+
+
+def test_concurrent_calls_are_batched():
+    holder = []
+    b = make_backend(holder=holder)
+    b.load_model(MID)
+    res = [None] * 16
+
+    def call(i):
+        res[i] = b.transcribe(wav(1.0 + 0.1 * i, i), MID)
+
+    ts = [threading.Thread(target=call, args=(i,)) for i in range(16)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert all(r is not None and "text" in r for r in res)
+    assert max(holder[0].batches) > 1          # at least one multi-request batch
+    b.unload_model(MID)
+
+
+def test_asyncio_executor_seam():
+    """main.transcribe runs the backend via loop.run_in_executor (src/main.py:305-315)."""
+    b = make_backend()
+
+    async def go():
+        loop = asyncio.get_running_loop()
+        return await asyncio.gather(*[loop.run_in_executor(None, lambda: b.transcribe(wav(1.0), MID))
+                                      for _ in range(4)])
+    out = asyncio.run(go())
+    assert len(out) == 4
+    b.unload_model(MID)
+
+
+def test_errors_propagate():
+    b = make_backend()
+    with pytest.raises(Exception):
+        b.transcribe(b"not audio at all", MID)
+    with pytest.raises(FileNotFoundError):
+        b.load_model("nonexistent-org/nonexistent-model")
+    b.unload_model(MID)
+
+
+class RouterStandIn:
+    """Mirror of BackendRouter's fields and dispatch (src/router.py:16-72)."""
+
+    def __init__(self):
+        self._backends = {"faster-whisper": object()}
+        self._default_backend = self._backends["faster-whisper"]
+
+    def get_backend(self, model_id):
+        return self._default_backend
+
+    def transcribe(self, audio, model, **kw):
+        return self.get_backend(model).transcribe(audio, model, **kw)
+
+
+def test_install_into_router_seam():
+    r = RouterStandIn()
+    b = install(r, make_backend())
+    assert r._backends["faster-whisper"] is b and r._default_backend is b
+    out = r.transcribe(wav(1.0), MID, language=None, response_format="json", temperature=0.0)
+    assert "text" in out
+    b.unload_model(MID)
+
+
+# --------------------------------------------------------------------------- audio ingest
+def _wav(x, sr, ch=1, width=2):
+    buf = io.BytesIO()
+    with wave.open(buf, "wb") as wf:
+        wf.setnchannels(ch)
+        wf.setsampwidth(width)
+        wf.setframerate(sr)
+        wf.writeframes(x.tobytes())
+    return buf.getvalue()
+
+
+def test_wav_16k_mono_exact():
+    pcm = synth.chirp_clip(3, 2.0)
+    assert np.array_equal(pcm16_from_wav(_wav(pcm, 16000)), pcm)
+
+
+def test_wav_stereo_and_resample():
+    x = (np.sin(np.arange(44100) * 2 * np.pi * 440 / 44100) * 8000).astype(np.int16)
+    st = np.stack([x, x], 1).reshape(-1)
+    y = pcm16_from_wav(_wav(st, 44100, ch=2))
+    assert abs(len(y) - 16000) <= 1 and y.dtype == np.int16
+    assert abs(np.abs(y).max() - 8000) < 400
+
+
+def test_non_wav_rejected_or_converted():
+    with pytest.raises(ValueError):
+        decode_audio_bytes(b"RIFF" + b"\x00" * 100)   # the reference tests' fake upload

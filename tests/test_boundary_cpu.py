@@ -41,3 +41,15 @@ def test_struct_sizes_match_header():
     assert ctypes.sizeof(_lib.osw_window) == 12
     assert ctypes.sizeof(_lib.osw_window_result) == 64
     assert ctypes.sizeof(_lib.osw_profile) == 8 * 18
+
+
+def test_product_path_has_no_cpu_fallback(tmp_path):
+    """With the library absent, loading fails loudly (no silent eager fallback)."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); import osw_path; osw_path.load();"
+            "from open_speech_amd import _lib\n"
+            "try:\n    _lib.load()\nexcept RuntimeError as e:\n    print('RAISED', e)\n") % ROOT
+    env = dict(__import__("os").environ, OSW_LIB=str(tmp_path / "missing.so"))
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert "RAISED" in out.stdout and "no CPU fallback" in out.stdout

@@ -70,7 +70,13 @@ def cpu_baseline(dims, n_tokens_per_clip: float, decode_steps: int) -> dict:
         cores = max((i.get("num_threads", 1) for i in threadpool_info()), default=1)
     except Exception:
         cores = os.cpu_count() or 1
-    w = weights.random_weights(dims, seed=0)
+    # same shapes/dtypes as the GPU run; values from a fast RNG (timing only)
+    rng = np.random.default_rng(0)
+    w = {}
+    for sp in weights.canonical_specs(dims):
+        shp = weights.spec_shape(sp, dims)
+        w[sp.name] = (rng.standard_normal(shp, dtype=np.float32) * 0.02).astype(
+            np.float16 if sp.dtype == weights.F16 else np.float32)
     orc = WhisperOracle(dims, w, fp16=False)
     del w
     st = D.SpecialTokens.for_vocab(dims.n_vocab)

@@ -133,6 +133,12 @@ int osw_transcribe_batch(osw_ctx* ctx, const int16_t* pcm, const int64_t* offset
 /* Parity helper: one encoder block on x [T][D] fp32 (host), result to y (host). */
 int osw_encoder_layer_debug(osw_ctx* ctx, int32_t layer, const float* x, float* y, int32_t T);
 
+/* Parity/timing helper: C[M][N] (fp32) = A[M][K] · W[N][K]ᵀ (fp16 host inputs) with GEMM
+ * variant 0 = auto, 1 = 128x128 tile, 2 = 256x256 tile, 3 = skinny split-K (M <= 64);
+ * runs `iters` times and stores the mean kernel time (ms, HIP events) in *ms. */
+int osw_debug_gemm(osw_ctx* ctx, int32_t M, int32_t N, int32_t K, int32_t variant, const void* A, const void* W,
+                   float* C, int32_t iters, float* ms);
+
 int osw_set_profiling(osw_ctx* ctx, int32_t enable);
 int osw_get_profile(osw_ctx* ctx, osw_profile* out);
 /* Device stream used by the context (hipStream_t as void*). */

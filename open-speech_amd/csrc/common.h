@@ -63,9 +63,11 @@ struct GemmArgs {
 
 // launchers (defined in the .hip files)
 void launch_gemm(const GemmArgs& g, hipStream_t s);
+void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s);  // 0 auto, 1 128-tile, 2 256-tile
 // M <= 64, K % 128 == 0; `part` needs skinny_ksplit(N,K)*M*N floats
 void launch_gemm_skinny(const GemmArgs& g, float* part, hipStream_t s);
 int skinny_ksplit(int N, int K);
+int launch_gemm_skinny_partial(const GemmArgs& g, float* part, hipStream_t s);
 void launch_layernorm(const float* x, int64_t M, int D, const float* g, const float* b, h16* y, hipStream_t s);
 
 }  // namespace osw

@@ -119,33 +119,134 @@ __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ 
     }
 }
 
-// grid (H, B): append this step's k,v to the cache, attend over positions 0..pos
-__global__ __launch_bounds__(256) void dec_self_attn_kernel(const h16* __restrict__ qkv, h16* __restrict__ kcache,
+// Sum the split-K partial slabs of a decoder projection for one (row, 64-column
+// head slice) and round to fp16 (the GEMM output precision the oracle emulates).
+// 256 threads: wave w sums slabs s = w, w+4, ... (independent loads in flight), then
+// lane d adds the 4 wave sums in fixed order (deterministic).
+__device__ __forceinline__ void reduce_head(const float* __restrict__ part, int ks, int64_t slab, int64_t off,
+                                            const float* __restrict__ bias, int col, h16* dst, float* red4) {
+    const int d = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float v = 0.f;
+    int s = w;
+    for (; s + 4 < ks; s += 8) v += part[s * slab + off + d] + part[(s + 4) * slab + off + d];
+    if (s < ks) v += part[s * slab + off + d];
+    red4[w * 64 + d] = v;
+    __syncthreads();
+    if (w == 0) {
+        float r = bias ? bias[col + d] : 0.f;
+        r += red4[d] + red4[64 + d] + red4[128 + d] + red4[192 + d];
+        dst[d] = (h16)r;
+    }
+    __syncthreads();
+}
+
+// grid (H, B): q,k,v = Σ split-K partials of the fused qkv projection + bias; k,v
+// appended to the cache at the device-side position; attend over 0..pos.
+__global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restrict__ part, int ks,
+                                                            const float* __restrict__ bias, h16* __restrict__ kcache,
                                                             h16* __restrict__ vcache, const int* __restrict__ pos_ptr,
-                                                            int H, int ctx, h16* __restrict__ out) {
+                                                            int H, int B, int ctx, h16* __restrict__ out) {
+    __shared__ h16 q16[HD];
+    __shared__ float red4[256];
     const int h = blockIdx.x, b = blockIdx.y;
     const int D = H * HD;
     const int pos = min(*pos_ptr, ctx - 1);  // graph replays may run past max_length on finished windows
-    const h16* row = qkv + (int64_t)b * 3 * D;
     h16* kc = kcache + ((int64_t)b * H + h) * ctx * HD;
     h16* vc = vcache + ((int64_t)b * H + h) * ctx * HD;
-    if (threadIdx.x < HD) {
-        kc[(int64_t)pos * HD + threadIdx.x] = row[D + h * HD + threadIdx.x];
-        vc[(int64_t)pos * HD + threadIdx.x] = row[2 * D + h * HD + threadIdx.x];
-    }
+    const int64_t slab = (int64_t)B * 3 * D, row = (int64_t)b * 3 * D;
+    reduce_head(part, ks, slab, row + h * HD, bias, h * HD, q16, red4);
+    reduce_head(part, ks, slab, row + D + h * HD, bias, D + h * HD, kc + (int64_t)pos * HD, red4);
+    reduce_head(part, ks, slab, row + 2 * D + h * HD, bias, 2 * D + h * HD, vc + (int64_t)pos * HD, red4);
     __threadfence_block();
     __syncthreads();
-    attend_one<448>(row + h * HD, kc, vc, pos + 1, out + (int64_t)b * D + h * HD);
+    attend_one<448>(q16, kc, vc, pos + 1, out + (int64_t)b * D + h * HD);
 }
 
-// grid (H, B): q [B][D]; xkv layer slice: K at ((0*nb + b)*H + h)*T*64, V at ((1*nb + b)*H + h)*T*64
-__global__ __launch_bounds__(256) void dec_cross_attn_kernel(const h16* __restrict__ q, const h16* __restrict__ xk,
-                                                             const h16* __restrict__ xv, int H, int T,
-                                                             h16* __restrict__ out) {
+// grid (H, B): q = Σ split-K partials of the cross-attention q projection + bias;
+// xkv layer slice: K at ((b*H + h)*T*64) of xk, V likewise of xv
+__global__ __launch_bounds__(256) void dec_cross_attn_kernel(const float* __restrict__ part, int ks,
+                                                             const float* __restrict__ bias,
+                                                             const h16* __restrict__ xk, const h16* __restrict__ xv,
+                                                             int H, int B, int T, h16* __restrict__ out) {
+    __shared__ h16 q16[HD];
+    __shared__ float red4[256];
     const int h = blockIdx.x, b = blockIdx.y;
     const int D = H * HD;
+    reduce_head(part, ks, (int64_t)B * D, (int64_t)b * D + h * HD, bias, h * HD, q16, red4);
     const int64_t hoff = ((int64_t)b * H + h) * T * HD;
-    attend_one<1536>(q + (int64_t)b * D + h * HD, xk + hoff, xv + hoff, T, out + (int64_t)b * D + h * HD);
+    attend_one<1536>(q16, xk + hoff, xv + hoff, T, out + (int64_t)b * D + h * HD);
+}
+
+// grid B, 1024 threads: x[b] += bias + Σ split-K partials (residual stream, fp32),
+// then LayerNorm(x[b]) -> y[b] fp16 (the next projection's operand).  Each thread
+// owns <= 2 columns and keeps 4 slab loads in flight.  With part == nullptr it is
+// the embedding entry: x[b] = tok_emb[tok[b]] + pos_emb[pos].
+__global__ __launch_bounds__(1024) void dec_resid_ln_kernel(const float* __restrict__ part, int ks, int B, int D,
+                                                            const float* __restrict__ bias, float* __restrict__ x,
+                                                            const float* __restrict__ g, const float* __restrict__ be,
+                                                            h16* __restrict__ y, const h16* __restrict__ tok_emb,
+                                                            const float* __restrict__ pos_emb,
+                                                            const int* __restrict__ tok,
+                                                            const int* __restrict__ pos_ptr, int ctx) {
+    __shared__ float red[16];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    constexpr int PER = 2;  // D <= 2048
+    float v[PER];
+    float s = 0.f;
+    const int64_t slab = (int64_t)B * D, rb = (int64_t)b * D;
+    int t = 0, pos = 0;
+    if (!part) {
+        t = tok[b];
+        pos = min(*pos_ptr, ctx - 1);
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int c = tid + 1024 * i;
+        float a = 0.f;
+        if (c < D) {
+            if (part) {
+                float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+                int k = 0;
+                for (; k + 3 < ks; k += 4) {
+                    a0 += part[(k + 0) * slab + rb + c];
+                    a1 += part[(k + 1) * slab + rb + c];
+                    a2 += part[(k + 2) * slab + rb + c];
+                    a3 += part[(k + 3) * slab + rb + c];
+                }
+                for (; k < ks; ++k) a0 += part[k * slab + rb + c];
+                a = x[rb + c] + (bias ? bias[c] : 0.f) + ((a0 + a1) + (a2 + a3));
+            } else {
+                a = (float)tok_emb[(int64_t)t * D + c] + pos_emb[(int64_t)pos * D + c];
+            }
+            x[rb + c] = a;
+        }
+        v[i] = a;
+        s += a;
+    }
+    const float mean = block_reduce_sum(s, red) / D;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int c = tid + 1024 * i;
+        if (c < D) q += (v[i] - mean) * (v[i] - mean);
+    }
+    const float rstd = rsqrtf(block_reduce_sum(q, red) / D + 1e-5f);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int c = tid + 1024 * i;
+        if (c < D) y[rb + c] = (h16)((v[i] - mean) * rstd * g[c] + be[c]);
+    }
+}
+
+// fc1: h[b][n] = fp16(gelu(bias + Σ partials))
+__global__ __launch_bounds__(256) void dec_reduce_gelu_kernel(const float* __restrict__ part, int ks, int64_t total,
+                                                              int N, const float* __restrict__ bias,
+                                                              h16* __restrict__ y) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        float v = bias[i % N];
+        for (int k = 0; k < ks; ++k) v += part[k * total + i];
+        y[i] = (h16)gelu_erf(v);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -337,13 +438,26 @@ __global__ void bump_kernel(int* p) { *p += 1; }
 
 int sel_state_bytes() { return (int)sizeof(SelState); }
 
-void launch_dec_self_attn(const h16* qkv, h16* kc, h16* vc, const int* pos, int B, int H, int ctx, h16* out,
-                          hipStream_t s) {
-    dec_self_attn_kernel<<<dim3(H, B), 256, 0, s>>>(qkv, kc, vc, pos, H, ctx, out);
+void launch_dec_self_attn(const float* part, int ks, const float* bias, h16* kc, h16* vc, const int* pos, int B,
+                          int H, int ctx, h16* out, hipStream_t s) {
+    dec_self_attn_kernel<<<dim3(H, B), 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out);
 }
 
-void launch_dec_cross_attn(const h16* q, const h16* xk, const h16* xv, int B, int H, int T, h16* out, hipStream_t s) {
-    dec_cross_attn_kernel<<<dim3(H, B), 256, 0, s>>>(q, xk, xv, H, T, out);
+void launch_dec_cross_attn(const float* part, int ks, const float* bias, const h16* xk, const h16* xv, int B, int H,
+                           int T, h16* out, hipStream_t s) {
+    dec_cross_attn_kernel<<<dim3(H, B), 256, 0, s>>>(part, ks, bias, xk, xv, H, B, T, out);
+}
+
+void launch_dec_resid_ln(const float* part, int ks, int B, int D, const float* bias, float* x, const float* g,
+                         const float* be, h16* y, const h16* tok_emb, const float* pos_emb, const int* tok,
+                         const int* pos, int ctx, hipStream_t s) {
+    dec_resid_ln_kernel<<<B, 1024, 0, s>>>(part, ks, B, D, bias, x, g, be, y, tok_emb, pos_emb, tok, pos, ctx);
+}
+
+void launch_dec_reduce_gelu(const float* part, int ks, int B, int N, const float* bias, h16* y, hipStream_t s) {
+    const int64_t total = (int64_t)B * N;
+    dec_reduce_gelu_kernel<<<(unsigned)std::min<int64_t>((total + 255) / 256, 1024), 256, 0, s>>>(part, ks, total, N,
+                                                                                                 bias, y);
 }
 
 void launch_select(const float* logits, int B, const int* pos, int prompt_len, int sot_pos, int lang_pos,

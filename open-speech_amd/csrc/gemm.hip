@@ -16,6 +16,8 @@
 // GEMM.  The C side has the same addressing.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace osw {
 
 namespace {
@@ -137,6 +139,301 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
         }
 }
 // ---------------------------------------------------------------------------
+// Large-M variant (encoder at batch >= ~8 windows): 256x256x64 tile, 8 waves (2 x 4),
+// each wave 128x64 = 8x4 MFMA tiles.  One K-step is 2048 MFMA cycles per SIMD
+// (~0.85 us), long enough to hide the one-tile-ahead global_load_lds prefetch that
+// the 128x128 tile (~0.2 us per K-step) cannot.  128 KiB LDS (2 stages) -> one
+// workgroup per CU.  Tiles are walked XCD-aware: the dispatcher deals workgroups
+// round-robin over the 8 XCDs, so id b is remapped to tile (b % 8)*ceil(n/8) + b/8
+// (bijective form) and each XCD's L2 sees a contiguous run of tiles that share
+// A row-panels.
+constexpr int GB = 256, GNT = 512;
+
+// LDS-staged epilogue for the 256x256 tile: the accumulators (bias / GELU / pos
+// applied) are written to an LDS image of the tile (rows padded so the MFMA-layout
+// writes are conflict-free), then every thread streams 16-B chunks to global —
+// 1 KiB contiguous per wave-instruction instead of 128 scattered 2/4-B stores per
+// lane.  fp32 tiles go through LDS in two 128-row halves.
+constexpr int EP16 = 264;  // fp16 row stride (halfs)
+constexpr int EP32 = 260;  // fp32 row stride (floats)
+constexpr int EPI_LDS = 256 * EP16 * 2;  // 135168 B >= 128 * EP32 * 4
+
+template <int EPI>
+__device__ __forceinline__ float epi_value(const GemmArgs& g, int m, int n, float v) {
+    if (g.bias) v += g.bias[n];
+    if constexpr (EPI == EPI_F16_GELU) v = gelu_erf(v);
+    return v;  // EPI_F32_GELU_POS: GELU + pos applied in the copy-out pass (fewer live registers)
+}
+
+template <int EPI>
+__device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], int m0, int n0, int wm,
+                                                int wn, char* smem) {
+    const int lane = threadIdx.x & 63, tid = threadIdx.x;
+    __syncthreads();
+    if constexpr (EPI == EPI_F16 || EPI == EPI_F16_GELU || EPI == EPI_HEADS) {
+        h16* T = (h16*)smem;
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int row = wm * 128 + mi * 16 + (lane >> 4) * 4 + i;
+                    const int col = wn * 64 + ni * 16 + (lane & 15);
+                    const int n = min(n0 + col, g.N - 1);
+                    T[row * EP16 + col] = (h16)epi_value<EPI>(g, m0 + row, n, acc[mi][ni][i]);
+                }
+        __syncthreads();
+#pragma unroll 4
+        for (int j = 0; j < 16; ++j) {
+            const int id = j * GNT + tid;
+            const int row = id >> 5, c8 = (id & 31) * 8;
+            const int m = m0 + row, n = n0 + c8;
+            if (m >= g.M || n >= g.N) continue;
+            const h16x8 v = *(const h16x8*)&T[row * EP16 + c8];
+            h16* dst;
+            if constexpr (EPI == EPI_HEADS) {
+                const int D = g.heads_H * 64;
+                const int which = n / D, h = (n % D) >> 6, d = n & 63;
+                const int b = m / g.heads_T, t = m % g.heads_T;
+                dst = (h16*)g.C + ((((int64_t)which * g.heads_nb + b) * g.heads_H + h) * g.heads_T + t) * 64 + d;
+            } else {
+                dst = (h16*)g.C + (m / g.c_grp_rows) * g.c_grp_stride + (int64_t)(m % g.c_grp_rows) * g.ldc + n;
+            }
+            *(h16x8*)dst = v;
+        }
+    } else {
+        float* T = (float*)smem;
+        for (int half = 0; half < 2; ++half) {
+            if (wm == half) {
+#pragma unroll
+                for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int row = mi * 16 + (lane >> 4) * 4 + i;
+                            const int col = wn * 64 + ni * 16 + (lane & 15);
+                            const int n = min(n0 + col, g.N - 1);
+                            T[row * EP32 + col] = epi_value<EPI>(g, m0 + half * 128 + row, n, acc[mi][ni][i]);
+                        }
+            }
+            __syncthreads();
+#pragma unroll 4
+            for (int j = 0; j < 16; ++j) {
+                const int id = j * GNT + tid;
+                const int row = id >> 6, c4 = (id & 63) * 4;
+                const int m = m0 + half * 128 + row, n = n0 + c4;
+                if (m < g.M && n < g.N) {
+                    f32x4 v = *(const f32x4*)&T[row * EP32 + c4];
+                    float* dst = (float*)g.C + (m / g.c_grp_rows) * g.c_grp_stride +
+                                 (int64_t)(m % g.c_grp_rows) * g.ldc + n;
+                    if constexpr (EPI == EPI_F32_RESID) v += *(const f32x4*)dst;
+                    if constexpr (EPI == EPI_F32_GELU_POS) {
+                        const f32x4 pv = *(const f32x4*)&g.pos[(int64_t)(m % g.c_grp_rows) * g.N + n];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]) + pv[e];
+                    }
+                    *(f32x4*)dst = v;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(GNT, 1) void gemm256_kernel(GemmArgs g) {
+    extern __shared__ __attribute__((aligned(16))) h16 smem[];  // [2][A|W][256*64]
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int ntn = (g.N + GB - 1) / GB, ntm = (g.M + GB - 1) / GB;
+    const int nwg = ntn * ntm;
+    const int bid = blockIdx.x;
+    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+    const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+    const int n0 = (tile % ntn) * GB, m0 = (tile / ntn) * GB;
+
+    const h16* asrc[4];
+    const h16* wsrc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int rr = (i * 8 + wave) * 8 + (lane >> 3);
+        const int c = swz(rr, lane & 7);
+        asrc[i] = grp_row(g.A, min(m0 + rr, g.M - 1), g.a_grp_rows, g.a_grp_stride, g.lda) + c * 8;
+        wsrc[i] = g.W + (int64_t)min(n0 + rr, g.N - 1) * g.ldw + c * 8;
+    }
+    auto stage = [&](int buf, int k0) {
+        h16* base = smem + buf * (2 * GB * BK);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int piece = i * 8 + wave;
+            __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + k0), (OSW_LDS void*)(base + piece * 8 * BK),
+                                             16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + k0),
+                                             (OSW_LDS void*)(base + GB * BK + piece * 8 * BK), 16, 0, 0);
+        }
+    };
+    const int wm = wave >> 2, wn = wave & 3;
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = g.K / BK;
+    stage(0, 0);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) stage(buf ^ 1, (kt + 1) * BK);
+        const h16* la = smem + buf * (2 * GB * BK);
+        const h16* lw = la + GB * BK;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int c = ks * 4 + (lane >> 4);
+            h16x8 b[4];
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) {
+                const int row = wn * 64 + ni * 16 + (lane & 15);
+                b[ni] = *(const h16x8*)&lw[row * BK + swz(row, c) * 8];
+            }
+#pragma unroll
+            for (int mi = 0; mi < 8; ++mi) {
+                const int row = wm * 128 + mi * 16 + (lane & 15);
+                const h16x8 a = *(const h16x8*)&la[row * BK + swz(row, c) * 8];
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni)
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[ni], acc[mi][ni], 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+    }
+    staged_epilogue<EPI>(g, acc, m0, n0, wm, wn, (char*)smem);
+}
+
+// 4-stage pipeline variant: BK = 32, three K-tiles in flight behind the one being
+// computed (counted vmcnt, raw s_barrier so the barrier does not drain the
+// global_load_lds queue; cdna_hip_programming.md §5 "Pipelining across barriers").
+// Rows are 64 B; the chunk swizzle c ^ (((row>>3)&1)*3) keeps the ds_read_b128
+// fragment reads conflict-free for the 16-lane groups of that instruction.
+constexpr int PBK = 32, PST = 4;
+__device__ __forceinline__ int swz32(int row, int chunk) { return chunk ^ (((row >> 3) & 1) * 3); }
+
+template <int EPI>
+__global__ __launch_bounds__(GNT, 1) void gemm256p_kernel(GemmArgs g) {
+    extern __shared__ __attribute__((aligned(16))) h16 smem[];  // [PST][A|W][256*32]
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int ntn = (g.N + GB - 1) / GB, ntm = (g.M + GB - 1) / GB;
+    const int nwg = ntn * ntm;
+    const int bid = blockIdx.x;
+    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+    const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+    const int n0 = (tile % ntn) * GB, m0 = (tile / ntn) * GB;
+
+    const h16* asrc[2];
+    const h16* wsrc[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int rr = (i * 8 + wave) * 16 + (lane >> 2);
+        const int c = swz32(rr, lane & 3);
+        asrc[i] = grp_row(g.A, min(m0 + rr, g.M - 1), g.a_grp_rows, g.a_grp_stride, g.lda) + c * 8;
+        wsrc[i] = g.W + (int64_t)min(n0 + rr, g.N - 1) * g.ldw + c * 8;
+    }
+    constexpr int STAGE = 2 * GB * PBK;  // halfs per stage
+    auto stage = [&](int buf, int k0) {
+        h16* base = smem + buf * STAGE;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int piece = i * 8 + wave;
+            __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + k0), (OSW_LDS void*)(base + piece * 16 * PBK),
+                                             16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + k0),
+                                             (OSW_LDS void*)(base + GB * PBK + piece * 16 * PBK), 16, 0, 0);
+        }
+    };
+    const int wm = wave >> 2, wn = wave & 3;
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = g.K / PBK;
+#pragma unroll
+    for (int t = 0; t < PST - 1; ++t)
+        if (t < nk) stage(t, t * PBK);
+    // tile 0 landed: every later tile issued so far may stay in flight
+    if (nk >= 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (nk == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const int c = lane >> 4;
+    for (int kt = 0; kt < nk; ++kt) {
+        if (kt + PST - 1 < nk) stage((kt + PST - 1) % PST, (kt + PST - 1) * PBK);
+        const h16* la = smem + (kt % PST) * STAGE;
+        const h16* lw = la + GB * PBK;
+        h16x8 b[4];
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+            const int row = wn * 64 + ni * 16 + (lane & 15);
+            b[ni] = *(const h16x8*)&lw[row * PBK + swz32(row, c) * 8];
+        }
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) {
+            const int row = wm * 128 + mi * 16 + (lane & 15);
+            const h16x8 a = *(const h16x8*)&la[row * PBK + swz32(row, c) * 8];
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+                acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[ni], acc[mi][ni], 0, 0, 0);
+        }
+        // tile kt+1 must have landed; tiles kt+2, kt+3 (4 glds each per wave) may stay in flight
+        const int ahead = min(nk - 1 - (kt + 1), PST - 2);
+        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    }
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int m = m0 + wm * 128 + mi * 16 + (lane >> 4) * 4 + i;
+            if (m >= g.M) continue;
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) {
+                const int n = n0 + wn * 64 + ni * 16 + (lane & 15);
+                if (n < g.N) store_one<EPI>(g, m, n, acc[mi][ni][i]);
+            }
+        }
+}
+
+template <int EPI>
+void launch256p(const GemmArgs& g, hipStream_t s) {
+    static bool attr = false;
+    constexpr int lds = PST * 2 * GB * PBK * 2;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)gemm256p_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        attr = true;
+    }
+    const int nwg = ((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
+    gemm256p_kernel<EPI><<<nwg, GNT, lds, s>>>(g);
+}
+
+template <int EPI>
+void launch256(const GemmArgs& g, hipStream_t s) {
+    static bool attr = false;
+    constexpr int lds = EPI_LDS > 2 * 2 * GB * BK * 2 ? EPI_LDS : 2 * 2 * GB * BK * 2;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        attr = true;
+    }
+    const int nwg = ((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
+    gemm256_kernel<EPI><<<nwg, GNT, lds, s>>>(g);
+}
+
+// ---------------------------------------------------------------------------
 // Skinny GEMM for the decoder (M <= 64 rows = windows in the batch): weight-
 // bandwidth bound, so the grid is split over N (64 columns per workgroup, 16 per
 // wave) AND over K (ksplit partial slabs, reduced deterministically by a second
@@ -144,7 +441,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
 // (no LDS: nothing is shared between waves but the tiny, L2-resident A).
 template <int MT, bool DIRECT, int EPI>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, float* __restrict__ part) {
-    constexpr int U = 4;
+    constexpr int U = 4;  // kc is a multiple of 128 = 32*U
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nb = blockIdx.x * 64 + wave * 16;
     const int ks = blockIdx.y;
@@ -234,6 +531,20 @@ int skinny_ksplit(int N, int K) {
     return best;
 }
 
+// partial-slab mode: always writes part[ks][M][N] (no epilogue); returns ksplit
+int launch_gemm_skinny_partial(const GemmArgs& g, float* part, hipStream_t s) {
+    const int ks = skinny_ksplit(g.N, g.K);
+    const dim3 grid((g.N + 63) / 64, ks);
+    const int kc = g.K / ks;
+    switch ((g.M + 15) / 16) {
+        case 1: gemm_skinny_kernel<1, false, EPI_F32><<<grid, 256, 0, s>>>(g, kc, part); break;
+        case 2: gemm_skinny_kernel<2, false, EPI_F32><<<grid, 256, 0, s>>>(g, kc, part); break;
+        case 3: gemm_skinny_kernel<3, false, EPI_F32><<<grid, 256, 0, s>>>(g, kc, part); break;
+        default: gemm_skinny_kernel<4, false, EPI_F32><<<grid, 256, 0, s>>>(g, kc, part); break;
+    }
+    return ks;
+}
+
 void launch_gemm_skinny(const GemmArgs& g, float* part, hipStream_t s) {
     const int ks = skinny_ksplit(g.N, g.K);
     switch (g.epi) {
@@ -245,7 +556,34 @@ void launch_gemm_skinny(const GemmArgs& g, float* part, hipStream_t s) {
     }
 }
 
-void launch_gemm(const GemmArgs& g, hipStream_t s) {
+void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s);
+
+void launch_gemm(const GemmArgs& g, hipStream_t s) { launch_gemm_variant(g, 0, s); }
+
+void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s) {
+    // big tile when it still yields >= 2 waves of workgroups over 256 CUs
+    const int64_t big_tiles = (int64_t)((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
+    const bool big = variant == 2 || (variant == 0 && big_tiles >= 512 && g.N % 8 == 0 && !getenv("OSW_GEMM128"));
+    if (variant == 4) {
+        switch (g.epi) {
+            case EPI_F16: launch256p<EPI_F16>(g, s); return;
+            case EPI_F16_GELU: launch256p<EPI_F16_GELU>(g, s); return;
+            case EPI_F32_RESID: launch256p<EPI_F32_RESID>(g, s); return;
+            case EPI_F32_GELU_POS: launch256p<EPI_F32_GELU_POS>(g, s); return;
+            case EPI_F32: launch256p<EPI_F32>(g, s); return;
+            default: launch256p<EPI_HEADS>(g, s); return;
+        }
+    }
+    if (big) {
+        switch (g.epi) {
+            case EPI_F16: launch256<EPI_F16>(g, s); return;
+            case EPI_F16_GELU: launch256<EPI_F16_GELU>(g, s); return;
+            case EPI_F32_RESID: launch256<EPI_F32_RESID>(g, s); return;
+            case EPI_F32_GELU_POS: launch256<EPI_F32_GELU_POS>(g, s); return;
+            case EPI_F32: launch256<EPI_F32>(g, s); return;
+            default: launch256<EPI_HEADS>(g, s); return;
+        }
+    }
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
     switch (g.epi) {
         case EPI_F16: gemm_kernel<EPI_F16><<<grid, NTHR, 0, s>>>(g); break;

@@ -31,8 +31,11 @@ void launch_enc_attn(const h16*, h16*, int, int, int, hipStream_t);
 void launch_init_uniform(void*, bool, int64_t, uint64_t, float, float, int64_t, int64_t, hipStream_t);
 uint64_t hash_stream_key(uint64_t, int64_t);
 void launch_dec_embed(const h16*, const float*, const int*, const int*, int, int, int, float*, hipStream_t);
-void launch_dec_self_attn(const h16*, h16*, h16*, const int*, int, int, int, h16*, hipStream_t);
-void launch_dec_cross_attn(const h16*, const h16*, const h16*, int, int, int, h16*, hipStream_t);
+void launch_dec_self_attn(const float*, int, const float*, h16*, h16*, const int*, int, int, int, h16*, hipStream_t);
+void launch_dec_cross_attn(const float*, int, const float*, const h16*, const h16*, int, int, int, h16*, hipStream_t);
+void launch_dec_resid_ln(const float*, int, int, int, const float*, float*, const float*, const float*, h16*,
+                         const h16*, const float*, const int*, const int*, int, hipStream_t);
+void launch_dec_reduce_gelu(const float*, int, int, int, const float*, h16*, hipStream_t);
 void launch_select(const float*, int, const int*, int, int, int, int, int, int, int, int, int, int, int, int, int, int,
                    int, const int*, const unsigned*, void*, int*, int*, int, hipStream_t);
 void launch_count_done(const void*, int, int*, hipStream_t);
@@ -508,37 +511,47 @@ void encode(osw_ctx* c, const osw_window* wins, int n) {
 }
 
 // ---------------------------- decoder --------------------------------------
+// One decoder step for nb windows.  Every projection is a split-K skinny GEMM whose
+// partial slabs are reduced by the kernel that consumes them (self/cross attention
+// for q/k/v, residual+LayerNorm for the out-projections and fc2, GELU for fc1).
 void decoder_step(osw_ctx* c, int nb) {
     const osw_dims& d = c->d;
-    const int D = d.n_text_state, H = d.n_text_head, L = d.n_text_layer;
+    const int D = d.n_text_state, H = d.n_text_head, L = d.n_text_layer, ctx = d.n_text_ctx;
     const int64_t xkv_which = (int64_t)nb * H * T_ENC * 64;
-    const int64_t kv_layer = (int64_t)nb * H * d.n_text_ctx * 64;
-    launch_dec_embed(WH(c, "dec.tok"), WF(c, "dec.pos"), c->cur_tok, c->pos, nb, D, d.n_text_ctx, c->xd, c->stream);
+    const int64_t kv_layer = (int64_t)nb * H * ctx * 64;
+    REQUIRE(nb <= 64 && D <= 1280, "decoder step: nb <= 64 and D <= 1280");
+    auto partial = [&](const h16* A, int lda, const h16* Wt, int N, int K) {
+        GemmArgs g = gemm_plain(A, lda, Wt, nullptr, nb, N, K, nullptr, 0, EPI_F32);
+        REQUIRE((int64_t)skinny_ksplit(N, K) * nb * N <= c->part_floats, "split-K workspace too small");
+        return launch_gemm_skinny_partial(g, c->part, c->stream);
+    };
+    // x = tok_emb[tok] + pos_emb[pos]; xdn = LN1_0(x)
+    launch_dec_resid_ln(nullptr, 0, nb, D, nullptr, c->xd, WF(c, "dec.l0.ln1.g"), WF(c, "dec.l0.ln1.b"), c->xdn,
+                        WH(c, "dec.tok"), WF(c, "dec.pos"), c->cur_tok, c->pos, ctx, c->stream);
     for (int l = 0; l < L; ++l) {
         const std::string p = "dec.l" + std::to_string(l);
-        launch_layernorm(c->xd, nb, D, WF(c, p + ".ln1.g"), WF(c, p + ".ln1.b"), c->xdn, c->stream);
-        run_gemm(c, gemm_plain(c->xdn, D, WH(c, p + ".qkv.w"), WF(c, p + ".qkv.b"), nb, 3 * D, D, c->dqkv, 3 * D,
-                               EPI_F16), 0);
-        launch_dec_self_attn(c->dqkv, c->kc + l * kv_layer, c->vc + l * kv_layer, c->pos, nb, H, d.n_text_ctx,
-                             c->dattn, c->stream);
-        run_gemm(c, gemm_plain(c->dattn, D, WH(c, p + ".o.w"), WF(c, p + ".o.b"), nb, D, D, c->xd, D, EPI_F32_RESID),
-                 0);
-        launch_layernorm(c->xd, nb, D, WF(c, p + ".ln2.g"), WF(c, p + ".ln2.b"), c->xdn, c->stream);
-        run_gemm(c, gemm_plain(c->xdn, D, WH(c, p + ".xq.w"), WF(c, p + ".xq.b"), nb, D, D, c->dq, D, EPI_F16), 0);
+        int ks = partial(c->xdn, D, WH(c, p + ".qkv.w"), 3 * D, D);
+        launch_dec_self_attn(c->part, ks, WF(c, p + ".qkv.b"), c->kc + l * kv_layer, c->vc + l * kv_layer, c->pos, nb,
+                             H, ctx, c->dattn, c->stream);
+        ks = partial(c->dattn, D, WH(c, p + ".o.w"), D, D);
+        launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".o.b"), c->xd, WF(c, p + ".ln2.g"), WF(c, p + ".ln2.b"),
+                            c->xdn, nullptr, nullptr, nullptr, nullptr, ctx, c->stream);
+        ks = partial(c->xdn, D, WH(c, p + ".xq.w"), D, D);
         {
             Timed t(c, CL_XATTN, 2.0 * nb * H * (double)T_ENC * 64 * 2);
-            launch_dec_cross_attn(c->dq, c->XKV + (2 * l) * xkv_which, c->XKV + (2 * l + 1) * xkv_which, nb, H, T_ENC,
-                                  c->dattn, c->stream);
+            launch_dec_cross_attn(c->part, ks, WF(c, p + ".xq.b"), c->XKV + (2 * l) * xkv_which,
+                                  c->XKV + (2 * l + 1) * xkv_which, nb, H, T_ENC, c->dattn, c->stream);
         }
-        run_gemm(c, gemm_plain(c->dattn, D, WH(c, p + ".xo.w"), WF(c, p + ".xo.b"), nb, D, D, c->xd, D,
-                               EPI_F32_RESID), 0);
-        launch_layernorm(c->xd, nb, D, WF(c, p + ".ln3.g"), WF(c, p + ".ln3.b"), c->xdn, c->stream);
-        run_gemm(c, gemm_plain(c->xdn, D, WH(c, p + ".fc1.w"), WF(c, p + ".fc1.b"), nb, 4 * D, D, c->dh, 4 * D,
-                               EPI_F16_GELU), 0);
-        run_gemm(c, gemm_plain(c->dh, 4 * D, WH(c, p + ".fc2.w"), WF(c, p + ".fc2.b"), nb, D, 4 * D, c->xd, D,
-                               EPI_F32_RESID), 0);
+        ks = partial(c->dattn, D, WH(c, p + ".xo.w"), D, D);
+        launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".xo.b"), c->xd, WF(c, p + ".ln3.g"), WF(c, p + ".ln3.b"),
+                            c->xdn, nullptr, nullptr, nullptr, nullptr, ctx, c->stream);
+        ks = partial(c->xdn, D, WH(c, p + ".fc1.w"), 4 * D, D);
+        launch_dec_reduce_gelu(c->part, ks, nb, 4 * D, WF(c, p + ".fc1.b"), c->dh, c->stream);
+        ks = partial(c->dh, 4 * D, WH(c, p + ".fc2.w"), D, 4 * D);
+        const std::string nx = l + 1 < L ? "dec.l" + std::to_string(l + 1) + ".ln1" : std::string("dec.lnpost");
+        launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".fc2.b"), c->xd, WF(c, nx + ".g"), WF(c, nx + ".b"), c->xdn,
+                            nullptr, nullptr, nullptr, nullptr, ctx, c->stream);
     }
-    launch_layernorm(c->xd, nb, D, WF(c, "dec.lnpost.g"), WF(c, "dec.lnpost.b"), c->xdn, c->stream);
     run_gemm(c, gemm_plain(c->xdn, D, WH(c, "dec.tok"), nullptr, nb, d.n_vocab, D, c->logits, d.n_vocab, EPI_F32), 0);
 }
 
@@ -953,6 +966,52 @@ int osw_encoder_layer_debug(osw_ctx* c, int32_t layer, const float* x, float* y,
         HIPCHK(hipMemcpyAsync(y, c->X, n * 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         resolve_events(c);
+    });
+}
+
+int osw_debug_gemm(osw_ctx* c, int32_t M, int32_t N, int32_t K, int32_t variant, const void* A, const void* Wt,
+                   float* C, int32_t iters, float* ms) {
+    return guard([&] {
+        REQUIRE(c && A && Wt && C && ms, "null argument");
+        REQUIRE(M >= 1 && N >= 1 && K >= 64 && K % 64 == 0 && iters >= 1, "bad GEMM shape");
+        REQUIRE(variant != 3 || (M <= 64 && K % 128 == 0), "skinny needs M <= 64 and K % 128 == 0");
+        std::lock_guard<std::mutex> lk(c->mu);
+        HIPCHK(hipSetDevice(c->device));
+        std::vector<void*> tmp;
+        h16* dA = dalloc<h16>((size_t)M * K, tmp);
+        h16* dW = dalloc<h16>((size_t)N * K, tmp);
+        float* dC = dalloc<float>((size_t)M * N, tmp);
+        float* dP = variant == 3 ? dalloc<float>((size_t)skinny_ksplit(N, K) * M * N, tmp) : nullptr;
+        hipEvent_t e0, e1;
+        HIPCHK(hipEventCreate(&e0));
+        HIPCHK(hipEventCreate(&e1));
+        try {
+            HIPCHK(hipMemcpy(dA, A, (size_t)M * K * 2, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(dW, Wt, (size_t)N * K * 2, hipMemcpyHostToDevice));
+            GemmArgs g = gemm_plain(dA, K, dW, nullptr, M, N, K, dC, N, EPI_F32);
+            auto run = [&] {
+                if (variant == 3) launch_gemm_skinny(g, dP, c->stream);
+                else launch_gemm_variant(g, variant, c->stream);
+            };
+            run();  // warm
+            HIPCHK(hipEventRecord(e0, c->stream));
+            for (int i = 0; i < iters; ++i) run();
+            HIPCHK(hipEventRecord(e1, c->stream));
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipEventSynchronize(e1));
+            float t = 0.f;
+            HIPCHK(hipEventElapsedTime(&t, e0, e1));
+            *ms = t / iters;
+            HIPCHK(hipMemcpy(C, dC, (size_t)M * N * 4, hipMemcpyDeviceToHost));
+        } catch (...) {
+            (void)hipEventDestroy(e0);
+            (void)hipEventDestroy(e1);
+            for (void* p : tmp) (void)hipFree(p);
+            throw;
+        }
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        for (void* p : tmp) (void)hipFree(p);
     });
 }
 

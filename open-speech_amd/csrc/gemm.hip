@@ -439,44 +439,118 @@ void launch256(const GemmArgs& g, hipStream_t s) {
 // wave) AND over K (ksplit partial slabs, reduced deterministically by a second
 // kernel that also applies the epilogue).  Operands go straight to VGPRs
 // (no LDS: nothing is shared between waves but the tiny, L2-resident A).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    // s_waitcnt vmcnt(N) with expcnt/lgkmcnt left at their maxima (gfx9 encoding)
+    static_assert(N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
 template <int MT, bool DIRECT, int EPI>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, float* __restrict__ part) {
-    constexpr int U = 4;  // kc is a multiple of 128 = 32*U
+    // Workgroup = 64 columns x one kc-deep K range; wave = 16 columns.  The
+    // activation rows (M <= 64) of each 256-deep K chunk are staged ONCE per
+    // workgroup into LDS by global_load_lds (row-XOR swizzle on the 16-B chunk ->
+    // conflict-free ds_read_b128), instead of every wave re-reading them from L2
+    // (4x the weight bytes at M = 64).  Weights stream straight to VGPRs, 8 x 16 B
+    // per lane per chunk, the next chunk's loads issued before the current chunk's
+    // MFMAs (two register sets, manual 2x unroll).  Loads are unconditional (clamped
+    // addresses for a short last chunk) so hipcc never branches around them.
+    constexpr int CK = 8;            // k32 steps per chunk (256 k)
+    constexpr int ROWS = MT * 16;
+    constexpr int APIECES = ROWS / 8;  // 1-KiB glds pieces per wave per chunk (2 rows each, 4 waves)
+    __shared__ __attribute__((aligned(16))) h16 As[2][ROWS * 256];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nb = blockIdx.x * 64 + wave * 16;
     const int ks = blockIdx.y;
     const int k0 = ks * kc;
     const int n = min(nb + (lane & 15), g.N - 1);
     const h16* wrow = g.W + (int64_t)n * g.ldw + k0 + 8 * (lane >> 4);
-    const h16* arow[MT];
+    const int nsteps = kc / 32;  // multiple of 4
+    const int nch = (nsteps + CK - 1) / CK;
+
+    const h16* asrc[APIECES];
+    int acl[APIECES];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-        const int m = min(mt * 16 + (lane & 15), g.M - 1);
-        arow[mt] = grp_row(g.A, m, g.a_grp_rows, g.a_grp_stride, g.lda) + k0 + 8 * (lane >> 4);
+    for (int i = 0; i < APIECES; ++i) {
+        const int j = i * 4 + wave;
+        const int row = 2 * j + (lane >> 5);
+        acl[i] = ((lane & 31) ^ (row & 15)) * 8;
+        asrc[i] = grp_row(g.A, min(row, g.M - 1), g.a_grp_rows, g.a_grp_stride, g.lda) + k0;
     }
+    auto stageA = [&](int buf, int c) {
+        // a short last chunk is staged from kc-256 so every load stays inside this K range;
+        // with kc < 256 the unused tail is clamped to the range's last 16 B (values unused)
+        const int kk = min(c * 256, kc - 256 > 0 ? kc - 256 : 0);
+#pragma unroll
+        for (int i = 0; i < APIECES; ++i) {
+            const int j = i * 4 + wave;
+            __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + min(kk + acl[i], kc - 8)),
+                                             (OSW_LDS void*)&As[buf][2 * j * 256], 16, 0, 0);
+        }
+    };
+    auto loadW = [&](h16x8 (&wf)[CK], int c) {
+#pragma unroll
+        for (int u = 0; u < CK; ++u) {
+            const int st = min(c * CK + u, nsteps - 1);
+            wf[u] = *(const h16x8*)(wrow + 32 * st);
+        }
+    };
     f32x4 acc[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < kc; k += 32 * U) {
-        h16x8 wf[U];
+    const int li = lane & 15, gq = lane >> 4;
+    auto consume = [&](const h16x8 (&wf)[CK], int buf, int c) {
+        const int steps = min(CK, nsteps - c * CK);
+        // a short last chunk was staged from kc-256: its k32 steps sit at the end of the image
+        const int shift = (c * 256 > kc - 256 && kc >= 256) ? (c * 256 - (kc - 256)) / 32 : 0;
 #pragma unroll
-        for (int u = 0; u < U; ++u) wf[u] = *(const h16x8*)(wrow + k + 32 * u);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
+        for (int u = 0; u < CK; ++u) {
+            if (u >= steps) break;
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) {
-                const h16x8 af = *(const h16x8*)(arow[mt] + k + 32 * u);
+                const int row = mt * 16 + li;
+                const int ch = ((u + shift) * 4 + gq) ^ (row & 15);
+                const h16x8 af = *(const h16x8*)&As[buf][row * 256 + ch * 8];
                 acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, wf[u], acc[mt], 0, 0, 0);
             }
         }
+    };
+    h16x8 wa[CK], wb[CK];
+    loadW(wa, 0);
+    stageA(0, 0);
+    for (int c = 0; c < nch; c += 2) {
+        if (c + 1 < nch) {
+            loadW(wb, c + 1);
+            stageA(1, c + 1);
+            wait_vmcnt<CK + APIECES>();
+        } else {
+            wait_vmcnt<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+        consume(wa, 0, c);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (c + 1 >= nch) break;
+        if (c + 2 < nch) {
+            loadW(wa, c + 2);
+            stageA(0, c + 2);
+            wait_vmcnt<CK + APIECES>();
+        } else {
+            wait_vmcnt<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+        consume(wb, 1, c + 1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
     }
-    const int col = nb + (lane & 15);
+    const int col = nb + li;
     if (col >= g.N) return;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int m = mt * 16 + (lane >> 4) * 4 + i;
+            const int m = mt * 16 + gq * 4 + i;
             if (m >= g.M) continue;
             if constexpr (DIRECT) store_one<EPI>(g, m, col, acc[mt][i]);
             else part[((int64_t)ks * g.M + m) * g.N + col] = acc[mt][i];
@@ -517,18 +591,17 @@ void skinny_mt(const GemmArgs& g, int ksplit, float* part, hipStream_t s) {
 }
 }  // namespace
 
-// split count: a divisor of K/128 giving 256..1024 workgroups when possible
+// split count: kc = 256 per workgroup (one register chunk of weights per wave)
+// when that gives <= 2048 workgroups, else the smallest larger power-of-two
+// multiple; K % 256 != 0 (small models) uses kc = 128.  Wide N (logits) runs
+// unsplit and streams its K in 256-deep chunks.
 int skinny_ksplit(int N, int K) {
     const int nbn = (N + 63) / 64;
-    const int kt = K / 128;
-    int best = 1;
-    for (int d = 1; d <= kt; ++d) {
-        if (kt % d) continue;
-        if ((int64_t)nbn * d > 1024) break;
-        best = d;
-        if ((int64_t)nbn * d >= 256) break;
-    }
-    return best;
+    if (nbn >= 512) return 1;
+    if (K % 256) return K / 128;
+    int kc = 256;
+    while ((K / kc) * nbn > 2048 && K % (2 * kc) == 0) kc *= 2;
+    return K / kc;
 }
 
 // partial-slab mode: always writes part[ks][M][N] (no epilogue); returns ksplit

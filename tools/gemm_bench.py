@@ -16,7 +16,9 @@ from open_speech_amd.engine import WhisperEngine  # noqa: E402
 SHAPES = [  # name, M, N, K, variants
     ("enc_qkv", 96000, 3840, 1280, (1, 2, 4)), ("enc_o", 96000, 1280, 1280, (1, 2, 4)),
     ("enc_fc1", 96000, 5120, 1280, (1, 2, 4)), ("enc_fc2", 96000, 1280, 5120, (1, 2, 4)),
-    ("dec_qkv", 64, 3840, 1280, (3,)), ("dec_fc2", 64, 1280, 5120, (3,)), ("dec_logits", 64, 51866, 1280, (3,)),
+    ("dec_qkv", 64, 3840, 1280, (3,)), ("dec_fc2", 64, 1280, 5120, (3,)), ("dec_o", 64, 1280, 1280, (3,)),
+    ("dec_qkv16", 16, 3840, 1280, (3,)), ("dec_logits", 64, 51866, 1280, (3, 1)), ("dec_logits32", 32, 51866, 1280, (3, 1)),
+    ("dec_logits16", 16, 51866, 1280, (3,)),
     ("dec_logits_b1", 1, 51866, 1280, (3,)), ("dec_fc1_b1", 1, 5120, 1280, (3,)),
 ]
 d = D.WhisperDims(n_mels=80, n_audio_state=128, n_audio_head=2, n_audio_layer=1, n_text_state=128, n_text_head=2,
@@ -24,7 +26,10 @@ d = D.WhisperDims(n_mels=80, n_audio_state=128, n_audio_head=2, n_audio_layer=1,
 eng = WhisperEngine(d, device=0, max_batch=1)
 rng = np.random.default_rng(0)
 out = []
+only = sys.argv[1] if len(sys.argv) > 1 else ""
 for name, M, N, K, vs in SHAPES:
+    if only and not name.startswith(only):
+        continue
     A = rng.uniform(-1, 1, (M, K)).astype(np.float16)
     W = rng.uniform(-1, 1, (N, K)).astype(np.float16)
     for v in vs:

@@ -115,7 +115,7 @@ class HipWhisperBackend:
             factory = self._engine_factory or _default_engine_factory
             engines = []
             try:
-                weights = model_store.load_hf_weights(src) if src.kind == "hf" else None
+                weights = model_store.load_weights(src)
                 for gpu in self._gpu_ids():
                     eng = factory(src.dims, gpu, max_batch)
                     if weights is not None:

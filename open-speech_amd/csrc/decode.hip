@@ -48,33 +48,34 @@ __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ 
     const int tid = threadIdx.x;
     if (tid < HD) qs[tid] = (float)q16[tid] * 0.125f;  // 1/sqrt(64), exact in fp32
     __syncthreads();
-    float q[HD];
+    // scores: 8 lanes per key row (lane c holds dims 8c..8c+7), so one wave-instruction
+    // reads 8 consecutive K rows = 1 KiB contiguous; 4 such loads in flight per lane;
+    // the 8-lane partial dots are combined with 3 xor-shuffles.
+    const int w = tid >> 6, kr = (tid >> 3) & 7, c8 = tid & 7;
+    float q[8];
 #pragma unroll
-    for (int i = 0; i < HD; ++i) q[i] = qs[i];
+    for (int i = 0; i < 8; ++i) q[i] = qs[8 * c8 + i];
     float mx = -INFINITY;
-    for (int j0 = tid; j0 < n_keys; j0 += 512) {
-        const int j1 = j0 + 256;
-        const bool two = j1 < n_keys;
-        const h16x8* k0 = (const h16x8*)(K + (int64_t)j0 * HD);
-        const h16x8* k1 = (const h16x8*)(K + (int64_t)(two ? j1 : j0) * HD);
-        h16x8 a[8], b[8];
+    for (int base = 0; base < n_keys; base += 128) {
+        h16x8 kv[4];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) a[c] = k0[c];
+        for (int u = 0; u < 4; ++u) {
+            const int key = min(base + u * 32 + w * 8 + kr, n_keys - 1);
+            kv[u] = *(const h16x8*)(K + (int64_t)key * HD + 8 * c8);
+        }
 #pragma unroll
-        for (int c = 0; c < 8; ++c) b[c] = k1[c];
-        float s0 = 0.f, s1 = 0.f;
+        for (int u = 0; u < 4; ++u) {
+            float d = 0.f;
 #pragma unroll
-        for (int c = 0; c < 8; ++c)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                s0 = fmaf((float)a[c][j], q[8 * c + j], s0);
-                s1 = fmaf((float)b[c][j], q[8 * c + j], s1);
+            for (int i = 0; i < 8; ++i) d = fmaf((float)kv[u][i], q[i], d);
+            d += __shfl_xor(d, 1, 64);
+            d += __shfl_xor(d, 2, 64);
+            d += __shfl_xor(d, 4, 64);
+            const int key = base + u * 32 + w * 8 + kr;
+            if (key < n_keys) {
+                if (c8 == 0) sc[key] = d;
+                mx = fmaxf(mx, d);
             }
-        sc[j0] = s0;
-        mx = fmaxf(mx, s0);
-        if (two) {
-            sc[j1] = s1;
-            mx = fmaxf(mx, s1);
         }
     }
     mx = block_reduce_max(mx, red);
@@ -289,72 +290,55 @@ __device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2
     else s += s2 * __expf(m2 - m);
 }
 
-__global__ __launch_bounds__(1024) void select_kernel(const float* __restrict__ logits, SelParams P,
-                                                      const int* __restrict__ pos_ptr,  // position just computed
-                                                      const int* __restrict__ prompt,   // [B][P] (-1 = detect)
-                                                      const unsigned* __restrict__ supmask,  // V bits
-                                                      SelState* __restrict__ st, int* __restrict__ cur_tok,
-                                                      int* __restrict__ tokens, int max_tokens) {
-    const int b = blockIdx.x;
-    const int tid = threadIdx.x;
-    const float* x = logits + (int64_t)b * P.V;
-    __shared__ float rm[16], rs[16], rm2[16], rs2[16];
-    __shared__ ArgMax ra[16], ra2[16], ra3[16];
-    SelState s = st[b];
-    const int w = tid >> 6, l = tid & 63;
+// Per-window statistics over one vocabulary slice, with the logits rules applied
+// on the fly (masked entries skipped):
+//   m_all/s_all : online log-sum-exp over the kept entries
+//   m_ts/s_ts   : the same over kept timestamp tokens
+//   a_all/a_text/a_ts : argmax (lowest index on ties) over kept / kept text / kept timestamps
+// At the <|startoftranscript|> step the slice stats are over the RAW logits and
+// a_text is the argmax over the language tokens (language id + no-speech prob).
+struct SelPart {
+    float m_all, s_all, m_ts, s_ts;
+    float v_all, v_text, v_ts;
+    int i_all, i_text, i_ts;
+};
+constexpr int SEL_SPLIT = 16;
+
+enum { SEL_PROMPT = 0, SEL_SOT = 1, SEL_SAMPLE = 2, SEL_DONE = 3 };
+
+__device__ __forceinline__ int sel_mode(const SelParams& P, int step, const SelState& s) {
+    if (step < P.prompt_len - 1) return step == P.sot_pos ? SEL_SOT : SEL_PROMPT;
+    return s.done ? SEL_DONE : SEL_SAMPLE;
+}
+
+// grid (B, SEL_SPLIT), 256 threads
+__global__ __launch_bounds__(256) void select_partial_kernel(const float* __restrict__ logits, SelParams P,
+                                                             const int* __restrict__ pos_ptr,
+                                                             const unsigned* __restrict__ supmask,
+                                                             const SelState* __restrict__ st,
+                                                             SelPart* __restrict__ parts) {
+    const int b = blockIdx.x, sl = blockIdx.y, tid = threadIdx.x;
     const int step = *pos_ptr;
-
-    if (step < P.prompt_len - 1) {
-        // prompt step: forced next token; SOT position -> no-speech prob (+ language detection)
-        int next = prompt[b * P.prompt_len + step + 1];
-        if (step == P.sot_pos) {
-            float m = -INFINITY, sum = 0.f;
-            ArgMax best{-INFINITY, 0x7fffffff};
-            for (int v = tid; v < P.V; v += blockDim.x) {
-                const float xv = x[v];
-                lse_add(m, sum, xv);
-                if (v >= P.first_lang && v < P.first_lang + P.n_langs) best = amax(best, ArgMax{xv, v});
-            }
-            // reduce
-            for (int o = 32; o > 0; o >>= 1) {
-                const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(sum, o, 64);
-                lse_merge(m, sum, m2, s2);
-                ArgMax bb{__shfl_xor(best.v, o, 64), __shfl_xor(best.i, o, 64)};
-                best = amax(best, bb);
-            }
-            if (l == 0) { rm[w] = m; rs[w] = sum; ra[w] = best; }
-            __syncthreads();
-            if (tid == 0) {
-                float M = rm[0], S = rs[0];
-                ArgMax B = ra[0];
-                for (int i = 1; i < (int)(blockDim.x >> 6); ++i) { lse_merge(M, S, rm[i], rs[i]); B = amax(B, ra[i]); }
-                const float lse = M + __logf(S);
-                s.nsp = __expf(x[P.no_speech] - lse);
-                if (next < 0) next = B.i;
-                s.lang = next;
-                st[b] = s;
-                cur_tok[b] = next;
-            }
-            return;
-        }
-        if (tid == 0) cur_tok[b] = next < 0 ? s.lang : next;
-        return;
-    }
-
-    if (s.done) {
-        if (tid == 0) cur_tok[b] = P.eot;
-        return;
-    }
-    // ---- sampling step: masks are applied on the fly
+    const SelState s = st[b];
+    const int mode = sel_mode(P, step, s);
+    if (mode == SEL_PROMPT || mode == SEL_DONE) return;
+    const float* x = logits + (int64_t)b * P.V;
+    const int per = (P.V + SEL_SPLIT - 1) / SEL_SPLIT;
+    const int lo = sl * per, hi = min(P.V, lo + per);
     const int n = s.n_sampled;
     const bool last_ts = n >= 1 && s.last >= P.tb;
     const bool pen_ts = n < 2 || s.penult >= P.tb;
-    int ts_lo_block = P.tb;  // timestamps in [tb, ts_min) are forbidden
-    if (P.with_ts && s.last_ts > 0) ts_lo_block = (last_ts && !pen_ts) ? s.last_ts : s.last_ts + 1;
+    int ts_block = P.tb;  // timestamps in [tb, ts_block) are forbidden (monotonicity)
+    if (P.with_ts && s.last_ts > 0) ts_block = (last_ts && !pen_ts) ? s.last_ts : s.last_ts + 1;
     float m_all = -INFINITY, s_all = 0.f, m_ts = -INFINITY, s_ts = 0.f;
     ArgMax a_all{-INFINITY, 0x7fffffff}, a_text{-INFINITY, 0x7fffffff}, a_ts{-INFINITY, 0x7fffffff};
-    for (int v = tid; v < P.V; v += blockDim.x) {
-        float xv = x[v];
+    for (int v = lo + tid; v < hi; v += 256) {
+        const float xv = x[v];
+        if (mode == SEL_SOT) {
+            lse_add(m_all, s_all, xv);
+            if (v >= P.first_lang && v < P.first_lang + P.n_langs) a_text = amax(a_text, ArgMax{xv, v});
+            continue;
+        }
         bool masked = (supmask[v >> 5] >> (v & 31)) & 1u;
         if (P.suppress_blank && n == 0 && (v == P.blank || v == P.eot)) masked = true;
         if (P.with_ts) {
@@ -363,7 +347,7 @@ __global__ __launch_bounds__(1024) void select_kernel(const float* __restrict__ 
                 if (pen_ts) { if (v >= P.tb) masked = true; }
                 else { if (v < P.eot) masked = true; }
             }
-            if (v >= P.tb && v < ts_lo_block) masked = true;
+            if (v >= P.tb && v < ts_block) masked = true;
             if (n == 0) {
                 if (v < P.tb) masked = true;
                 if (P.max_init_ts >= 0 && v > P.tb + P.max_init_ts) masked = true;
@@ -382,48 +366,98 @@ __global__ __launch_bounds__(1024) void select_kernel(const float* __restrict__ 
     for (int o = 32; o > 0; o >>= 1) {
         float m2 = __shfl_xor(m_all, o, 64), s2 = __shfl_xor(s_all, o, 64);
         lse_merge(m_all, s_all, m2, s2);
-        m2 = __shfl_xor(m_ts, o, 64); s2 = __shfl_xor(s_ts, o, 64);
+        m2 = __shfl_xor(m_ts, o, 64);
+        s2 = __shfl_xor(s_ts, o, 64);
         lse_merge(m_ts, s_ts, m2, s2);
         a_all = amax(a_all, ArgMax{__shfl_xor(a_all.v, o, 64), __shfl_xor(a_all.i, o, 64)});
         a_text = amax(a_text, ArgMax{__shfl_xor(a_text.v, o, 64), __shfl_xor(a_text.i, o, 64)});
         a_ts = amax(a_ts, ArgMax{__shfl_xor(a_ts.v, o, 64), __shfl_xor(a_ts.i, o, 64)});
     }
-    if (l == 0) { rm[w] = m_all; rs[w] = s_all; rm2[w] = m_ts; rs2[w] = s_ts; ra[w] = a_all; ra2[w] = a_text; ra3[w] = a_ts; }
+    __shared__ SelPart wp[4];
+    const int w = tid >> 6;
+    if ((tid & 63) == 0) wp[w] = SelPart{m_all, s_all, m_ts, s_ts, a_all.v, a_text.v, a_ts.v, a_all.i, a_text.i, a_ts.i};
     __syncthreads();
     if (tid == 0) {
-        float MA = rm[0], SA = rs[0], MT = rm2[0], ST = rs2[0];
-        ArgMax A = ra[0], AX = ra2[0], AT = ra3[0];
-        for (int i = 1; i < (int)(blockDim.x >> 6); ++i) {
-            lse_merge(MA, SA, rm[i], rs[i]);
-            lse_merge(MT, ST, rm2[i], rs2[i]);
-            A = amax(A, ra[i]); AX = amax(AX, ra2[i]); AT = amax(AT, ra3[i]);
+        SelPart r = wp[0];
+        for (int i = 1; i < 4; ++i) {
+            const SelPart& q = wp[i];
+            lse_merge(r.m_all, r.s_all, q.m_all, q.s_all);
+            lse_merge(r.m_ts, r.s_ts, q.m_ts, q.s_ts);
+            ArgMax A = amax(ArgMax{r.v_all, r.i_all}, ArgMax{q.v_all, q.i_all});
+            ArgMax X = amax(ArgMax{r.v_text, r.i_text}, ArgMax{q.v_text, q.i_text});
+            ArgMax T = amax(ArgMax{r.v_ts, r.i_ts}, ArgMax{q.v_ts, q.i_ts});
+            r.v_all = A.v; r.i_all = A.i; r.v_text = X.v; r.i_text = X.i; r.v_ts = T.v; r.i_ts = T.i;
         }
-        const float lse_all = MA + __logf(SA);
-        int next = A.i;
-        float lp = A.v - lse_all;
-        if (P.with_ts) {
-            const float lse_ts = MT == -INFINITY ? -INFINITY : MT + __logf(ST);
-            const float ts_lp = lse_ts - lse_all;
-            const float text_lp = AX.v - lse_all;
-            if (ts_lp > text_lp) {  // timestamp mass wins: text suppressed, renormalise over timestamps
-                next = AT.i;
-                lp = AT.v - lse_ts;
-            }
-        }
-        s.sum_lp += lp;
-        if (next == P.eot) {
-            s.done = 1;
-        } else {
-            if (n < max_tokens) tokens[(int64_t)b * max_tokens + n] = next;
-            s.n_sampled = n + 1;
-            s.penult = s.last;
-            s.last = next;
-            if (next >= P.tb) s.last_ts = next;
-            if (P.prompt_len + s.n_sampled >= P.max_length) s.done = 1;
-        }
+        parts[b * SEL_SPLIT + sl] = r;
+    }
+}
+
+// grid B, 64 threads: combine the slices in fixed order, apply the timestamp-mass
+// rule, pick the token, update the window state.
+__global__ __launch_bounds__(64) void select_final_kernel(const float* __restrict__ logits, SelParams P,
+                                                          const int* __restrict__ pos_ptr,
+                                                          const int* __restrict__ prompt,  // [B][P] (-1 = detect)
+                                                          const SelPart* __restrict__ parts,
+                                                          SelState* __restrict__ st, int* __restrict__ cur_tok,
+                                                          int* __restrict__ tokens, int max_tokens) {
+    const int b = blockIdx.x;
+    if (threadIdx.x != 0) return;
+    const int step = *pos_ptr;
+    SelState s = st[b];
+    const int mode = sel_mode(P, step, s);
+    if (mode == SEL_PROMPT) {
+        const int next = prompt[b * P.prompt_len + step + 1];
+        cur_tok[b] = next < 0 ? s.lang : next;
+        return;
+    }
+    if (mode == SEL_DONE) {
+        cur_tok[b] = P.eot;
+        return;
+    }
+    SelPart r = parts[b * SEL_SPLIT];
+    for (int i = 1; i < SEL_SPLIT; ++i) {
+        const SelPart& q = parts[b * SEL_SPLIT + i];
+        lse_merge(r.m_all, r.s_all, q.m_all, q.s_all);
+        lse_merge(r.m_ts, r.s_ts, q.m_ts, q.s_ts);
+        ArgMax A = amax(ArgMax{r.v_all, r.i_all}, ArgMax{q.v_all, q.i_all});
+        ArgMax X = amax(ArgMax{r.v_text, r.i_text}, ArgMax{q.v_text, q.i_text});
+        ArgMax T = amax(ArgMax{r.v_ts, r.i_ts}, ArgMax{q.v_ts, q.i_ts});
+        r.v_all = A.v; r.i_all = A.i; r.v_text = X.v; r.i_text = X.i; r.v_ts = T.v; r.i_ts = T.i;
+    }
+    const float lse_all = r.m_all + __logf(r.s_all);
+    if (mode == SEL_SOT) {
+        const float* x = logits + (int64_t)b * P.V;
+        s.nsp = __expf(x[P.no_speech] - lse_all);
+        int next = prompt[b * P.prompt_len + step + 1];
+        if (next < 0) next = r.i_text;  // language detection: argmax over language tokens
+        s.lang = next;
         st[b] = s;
         cur_tok[b] = next;
+        return;
     }
+    const int n = s.n_sampled;
+    int next = r.i_all;
+    float lp = r.v_all - lse_all;
+    if (P.with_ts) {
+        const float lse_ts = r.m_ts == -INFINITY ? -INFINITY : r.m_ts + __logf(r.s_ts);
+        if (lse_ts - lse_all > r.v_text - lse_all) {  // timestamp mass wins: text suppressed
+            next = r.i_ts;
+            lp = r.v_ts - lse_ts;
+        }
+    }
+    s.sum_lp += lp;
+    if (next == P.eot) {
+        s.done = 1;
+    } else {
+        if (n < max_tokens) tokens[(int64_t)b * max_tokens + n] = next;
+        s.n_sampled = n + 1;
+        s.penult = s.last;
+        s.last = next;
+        if (next >= P.tb) s.last_ts = next;
+        if (P.prompt_len + s.n_sampled >= P.max_length) s.done = 1;
+    }
+    st[b] = s;
+    cur_tok[b] = next;
 }
 
 __global__ void count_done_kernel(const SelState* st, int B, int* out) {
@@ -437,6 +471,7 @@ __global__ void bump_kernel(int* p) { *p += 1; }
 }  // namespace
 
 int sel_state_bytes() { return (int)sizeof(SelState); }
+int sel_parts_bytes() { return (int)sizeof(SelPart) * SEL_SPLIT; }
 
 void launch_dec_self_attn(const float* part, int ks, const float* bias, h16* kc, h16* vc, const int* pos, int B,
                           int H, int ctx, h16* out, hipStream_t s) {
@@ -463,10 +498,14 @@ void launch_dec_reduce_gelu(const float* part, int ks, int B, int N, const float
 void launch_select(const float* logits, int B, const int* pos, int prompt_len, int sot_pos, int lang_pos,
                    int max_length, int V, int eot, int no_speech, int no_ts, int tb, int blank, int first_lang,
                    int n_langs, int suppress_blank, int with_ts, int max_init_ts, const int* prompt,
-                   const unsigned* supmask, void* st, int* cur_tok, int* tokens, int max_tokens, hipStream_t s) {
+                   const unsigned* supmask, void* st, int* cur_tok, int* tokens, int max_tokens, void* sel_parts,
+                   hipStream_t s) {
     SelParams P{prompt_len, sot_pos, lang_pos, max_length, V, eot, no_speech, no_ts, tb, blank, first_lang,
                 n_langs, suppress_blank, with_ts, max_init_ts};
-    select_kernel<<<B, 1024, 0, s>>>(logits, P, pos, prompt, supmask, (SelState*)st, cur_tok, tokens, max_tokens);
+    select_partial_kernel<<<dim3(B, SEL_SPLIT), 256, 0, s>>>(logits, P, pos, supmask, (const SelState*)st,
+                                                              (SelPart*)sel_parts);
+    select_final_kernel<<<B, 64, 0, s>>>(logits, P, pos, prompt, (const SelPart*)sel_parts, (SelState*)st, cur_tok,
+                                          tokens, max_tokens);
 }
 
 void launch_count_done(const void* st, int B, int* out, hipStream_t s) {

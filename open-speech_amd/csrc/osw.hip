@@ -37,7 +37,8 @@ void launch_dec_resid_ln(const float*, int, int, int, const float*, float*, cons
                          const h16*, const float*, const int*, const int*, int, hipStream_t);
 void launch_dec_reduce_gelu(const float*, int, int, int, const float*, h16*, hipStream_t);
 void launch_select(const float*, int, const int*, int, int, int, int, int, int, int, int, int, int, int, int, int, int,
-                   int, const int*, const unsigned*, void*, int*, int*, int, hipStream_t);
+                   int, const int*, const unsigned*, void*, int*, int*, int, void*, hipStream_t);
+int sel_parts_bytes();
 void launch_count_done(const void*, int, int*, hipStream_t);
 void launch_bump(int*, hipStream_t);
 int sel_state_bytes();
@@ -150,6 +151,7 @@ struct osw_ctx {
     int *cur_tok = nullptr, *pos = nullptr, *tokens = nullptr, *prompt = nullptr, *done = nullptr;
     unsigned* supmask = nullptr;
     void* sel = nullptr;
+    void* selp = nullptr;      // per-window vocabulary-slice partial stats
     int* done_host = nullptr;  // pinned
     float* part = nullptr;     // split-K partial slabs of the decoder GEMMs
     int64_t part_floats = 0;
@@ -401,6 +403,7 @@ void setup_workspace(osw_ctx* c) {
     c->done = dalloc<int>(1, o);
     c->supmask = dalloc<unsigned>((d.n_vocab + 31) / 32, o);
     c->sel = dalloc<char>((size_t)B * sel_state_bytes(), o);
+    c->selp = dalloc<char>((size_t)B * sel_parts_bytes(), o);
     {
         const int64_t Bm = std::min<int64_t>(B, 64);
         const int64_t shapes[][2] = {{3 * Dd, Dd}, {Dd, Dd}, {4 * Dd, Dd}, {Dd, 4 * Dd}, {d.n_vocab, Dd}};
@@ -596,7 +599,7 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
         launch_select(c->logits, nb, c->pos, P, n_pre, n_pre + 1, max_len, V, o->eot, o->no_speech,
                       o->no_timestamps, o->timestamp_begin, o->blank, o->first_lang, o->n_langs, o->suppress_blank,
                       o->without_timestamps ? 0 : 1, o->max_initial_timestamp_index, c->prompt, c->supmask, c->sel,
-                      c->cur_tok, c->tokens, max_tok, c->stream);
+                      c->cur_tok, c->tokens, max_tok, c->selp, c->stream);
         launch_bump(c->pos, c->stream);
     };
     const int CH = 8;
@@ -651,7 +654,8 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
                     launch_select(c->logits, nb, c->pos, P, n_pre, n_pre + 1, max_len, V, o->eot, o->no_speech,
                                   o->no_timestamps, o->timestamp_begin, o->blank, o->first_lang, o->n_langs,
                                   o->suppress_blank, o->without_timestamps ? 0 : 1, o->max_initial_timestamp_index,
-                                  c->prompt, c->supmask, c->sel, c->cur_tok, c->tokens, max_tok, c->stream);
+                                  c->prompt, c->supmask, c->sel, c->cur_tok, c->tokens, max_tok, c->selp,
+                                  c->stream);
                     launch_bump(c->pos, c->stream);
                 } else {
                     one_step();

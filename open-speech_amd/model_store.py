@@ -10,9 +10,10 @@ Supported on-disk formats:
 * ``random:<preset>[:<seed>]`` — deterministic random weights at a preset's dims
   (``large-v3-turbo``, ``tiny-test``, ``micro-test``) for benchmarking and tests.
 
-CTranslate2 ``model.bin`` directories (the reference's default
-``deepdml/faster-whisper-large-v3-turbo-ct2``) are detected and rejected with a
-clear message: that loader is the next §8(f) row.  Nothing here downloads.
+* a CTranslate2 directory: ``model.bin`` (+ ``tokenizer.json``) — the format of the
+  reference's default ``deepdml/faster-whisper-large-v3-turbo-ct2`` (``ct2.py``).
+
+Nothing here downloads.
 """
 from __future__ import annotations
 
@@ -31,7 +32,7 @@ from .weights import dims_from_hf_config, from_hf_state_dict
 class ModelSource:
     model_id: str
     dims: WhisperDims
-    kind: str               # "random" | "hf"
+    kind: str               # "random" | "hf" | "ct2"
     path: str | None = None
     seed: int = 0
     tokenizer_json: str | None = None
@@ -77,12 +78,27 @@ def resolve(model_id: str, model_dir: str | None = None) -> ModelSource:
             with open(cfg) as fh:
                 dims = dims_from_hf_config(json.load(fh))
             return ModelSource(model_id, dims, "hf", path=d, tokenizer_json=tok if os.path.exists(tok) else None)
-        if os.path.exists(os.path.join(d, "model.bin")):
-            raise NotImplementedError(
-                f"{d} is a CTranslate2 model.bin; this backend loads transformers checkpoints "
-                "(config.json + model.safetensors). Convert it or point STT_MODEL at a transformers Whisper.")
+        mb = os.path.join(d, "model.bin")
+        if os.path.exists(mb):
+            from .ct2 import dims_from_ct2, read_model_bin
+
+            v, _ = read_model_bin(mb)
+            return ModelSource(model_id, dims_from_ct2(v), "ct2", path=d,
+                               tokenizer_json=tok if os.path.exists(tok) else None)
     raise FileNotFoundError(f"model {model_id!r} not found locally (searched {cache_dirs(model_dir)}); "
                             "this backend never downloads")
+
+
+def load_weights(src: ModelSource) -> dict | None:
+    """Canonical weights for a resolved source (None for random init)."""
+    if src.kind == "hf":
+        return load_hf_weights(src)
+    if src.kind == "ct2":
+        from .ct2 import ct2_to_canonical, read_model_bin
+
+        v, aliases = read_model_bin(os.path.join(src.path, "model.bin"))
+        return ct2_to_canonical(v, aliases, src.dims)
+    return None
 
 
 def load_hf_weights(src: ModelSource) -> dict:

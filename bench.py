@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--latency-repeats", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-decode-steps", type=int, default=8)
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc_encoder.json"),
+                    help="per-kernel HBM bytes from a rocprofv3 --pmc pass (tools/pmc_summary.py)")
     return ap.parse_args()
 
 
@@ -180,6 +182,15 @@ def main():
             roof = {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
         roof["avg_launch_ms"] = round(ms / max(1, nl), 4)
+        roof["work_per_launch"] = work / max(1, nl)
+        try:
+            with open(a.pmc_summary) as fh:
+                pmc = json.load(fh)["classes"].get(name)
+            if pmc:
+                roof["traffic"] = round(pmc["hbm_bytes_per_launch"])
+                roof["traffic_source"] = os.path.relpath(a.pmc_summary, ROOT)
+        except (OSError, KeyError, ValueError):
+            pass
         stages = {k: {"ms": round(v[0], 2), "launches": int(v[2])} for k, v in cands.items()}
 
         # p50 latency at batch 1 (BASELINE configs[1])

@@ -38,8 +38,16 @@ __global__ __launch_bounds__(256, 2) void enc_attn_kernel(const h16* __restrict_
     __shared__ __attribute__((aligned(16))) h16 lds[2][2][KB * HD];  // [buf][K|V] 32 KiB
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g = lane >> 4, li = lane & 15;
-    const int h = blockIdx.y, b = blockIdx.z;
-    const int q0 = blockIdx.x * QB + wave * 32;
+    // XCD-aware order: the dispatcher deals workgroups round-robin over 8 XCDs; remap
+    // (bijectively) so each XCD walks a contiguous run of (q-block, head, window)
+    // indices with the q-block fastest -> one head's K/V stays in one XCD's L2.
+    const int nqb = gridDim.x;
+    const int nwg = nqb * gridDim.y * gridDim.z;
+    const int bid = blockIdx.x + nqb * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int qq = nwg / 8, rr = nwg % 8, xcd = bid % 8;
+    const int lin = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + bid / 8;
+    const int qb = lin % nqb, h = (lin / nqb) % H, b = lin / (nqb * H);
+    const int q0 = qb * QB + wave * 32;
     const int64_t head_elems = (int64_t)T * HD;
     const h16* Qh = qkv + (((int64_t)0 * nb + b) * H + h) * head_elems;
     const h16* Kh = qkv + (((int64_t)1 * nb + b) * H + h) * head_elems;

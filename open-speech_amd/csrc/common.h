@@ -59,6 +59,7 @@ struct GemmArgs {
     const float* pos;                    // EPI_F32_GELU_POS: pos[(m % c_grp_rows)][n]
     int epi;
     int heads_T, heads_H, heads_nb;      // EPI_HEADS geometry
+    int band;                            // 256-tile walk: column band width (0 = all columns)
 };
 
 // launchers (defined in the .hip files)

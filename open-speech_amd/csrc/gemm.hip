@@ -165,7 +165,14 @@ __device__ __forceinline__ float epi_value(const GemmArgs& g, int m, int n, floa
     return v;  // EPI_F32_GELU_POS: GELU + pos applied in the copy-out pass (fewer live registers)
 }
 
-template <int EPI>
+// IL = false: wave (wm, wn) owns rows wm*128 + [0,128) and cols wn*64 + [0,64).
+// IL = true (8-phase kernel): rows {0,128} + wm*64 + [0,64), cols {0,128} + wn*32 + [0,32).
+template <bool IL>
+__device__ __forceinline__ int acc_row(int wm, int mi) { return IL ? (mi >> 2) * 128 + wm * 64 + (mi & 3) * 16 : wm * 128 + mi * 16; }
+template <bool IL>
+__device__ __forceinline__ int acc_col(int wn, int ni) { return IL ? (ni >> 1) * 128 + wn * 32 + (ni & 1) * 16 : wn * 64 + ni * 16; }
+
+template <int EPI, bool IL = false>
 __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], int m0, int n0, int wm,
                                                 int wn, char* smem) {
     const int lane = threadIdx.x & 63, tid = threadIdx.x;
@@ -178,8 +185,8 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
             for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const int row = wm * 128 + mi * 16 + (lane >> 4) * 4 + i;
-                    const int col = wn * 64 + ni * 16 + (lane & 15);
+                    const int row = acc_row<IL>(wm, mi) + (lane >> 4) * 4 + i;
+                    const int col = acc_col<IL>(wn, ni) + (lane & 15);
                     const int n = min(n0 + col, g.N - 1);
                     T[row * EP16 + col] = (h16)epi_value<EPI>(g, m0 + row, n, acc[mi][ni][i]);
                 }
@@ -205,15 +212,16 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
     } else {
         float* T = (float*)smem;
         for (int half = 0; half < 2; ++half) {
-            if (wm == half) {
+            if (IL || wm == half) {
 #pragma unroll
                 for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
                     for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
                         for (int i = 0; i < 4; ++i) {
-                            const int row = mi * 16 + (lane >> 4) * 4 + i;
-                            const int col = wn * 64 + ni * 16 + (lane & 15);
+                            if (IL && (mi >> 2) != half) continue;
+                            const int row = acc_row<IL>(wm, mi) - half * 128 + (lane >> 4) * 4 + i;
+                            const int col = acc_col<IL>(wn, ni) + (lane & 15);
                             const int n = min(n0 + col, g.N - 1);
                             T[row * EP32 + col] = epi_value<EPI>(g, m0 + half * 128 + row, n, acc[mi][ni][i]);
                         }
@@ -251,7 +259,13 @@ __global__ __launch_bounds__(GNT, 1) void gemm256_kernel(GemmArgs g) {
     const int bid = blockIdx.x;
     const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
     const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
-    const int n0 = (tile % ntn) * GB, m0 = (tile / ntn) * GB;
+    // column bands of G tiles: consecutive tiles sweep G columns of one row panel, then
+    // the next row panel, so an XCD keeps G weight panels L2-hot while A panels stream
+    // (G chosen on the host to minimise A*ntn/G + W*ntm*G/32 bytes of L2 misses)
+    const int G = g.band > 0 ? min(g.band, ntn) : ntn;
+    const int band = tile / (G * ntm), rr0 = tile % (G * ntm);
+    const int gw = min(G, ntn - band * G);
+    const int n0 = (band * G + rr0 % gw) * GB, m0 = (rr0 / gw) * GB;
 
     const h16* asrc[4];
     const h16* wsrc[4];
@@ -313,125 +327,203 @@ __global__ __launch_bounds__(GNT, 1) void gemm256_kernel(GemmArgs g) {
     staged_epilogue<EPI>(g, acc, m0, n0, wm, wn, (char*)smem);
 }
 
-// 4-stage pipeline variant: BK = 32, three K-tiles in flight behind the one being
-// computed (counted vmcnt, raw s_barrier so the barrier does not drain the
-// global_load_lds queue; cdna_hip_programming.md §5 "Pipelining across barriers").
-// Rows are 64 B; the chunk swizzle c ^ (((row>>3)&1)*3) keeps the ds_read_b128
-// fragment reads conflict-free for the 16-lane groups of that instruction.
-constexpr int PBK = 32, PST = 4;
-__device__ __forceinline__ int swz32(int row, int chunk) { return chunk ^ (((row >> 3) & 1) * 3); }
-
-template <int EPI>
-__global__ __launch_bounds__(GNT, 1) void gemm256p_kernel(GemmArgs g) {
-    extern __shared__ __attribute__((aligned(16))) h16 smem[];  // [PST][A|W][256*32]
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+// band width minimising modelled L2-miss bytes: A re-read once per band, a band's
+// weights re-read once per 32/G concurrently resident row panels of an XCD
+int choose_band(const GemmArgs& g) {
+    if (const char* e = getenv("OSW_GEMM_BAND")) return atoi(e);
     const int ntn = (g.N + GB - 1) / GB, ntm = (g.M + GB - 1) / GB;
-    const int nwg = ntn * ntm;
-    const int bid = blockIdx.x;
-    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
-    const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
-    const int n0 = (tile % ntn) * GB, m0 = (tile / ntn) * GB;
-
-    const h16* asrc[2];
-    const h16* wsrc[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int rr = (i * 8 + wave) * 16 + (lane >> 2);
-        const int c = swz32(rr, lane & 3);
-        asrc[i] = grp_row(g.A, min(m0 + rr, g.M - 1), g.a_grp_rows, g.a_grp_stride, g.lda) + c * 8;
-        wsrc[i] = g.W + (int64_t)min(n0 + rr, g.N - 1) * g.ldw + c * 8;
+    const double abytes = (double)g.M * g.K * 2, wbytes = (double)g.N * g.K * 2;
+    int best = ntn;
+    double bc = 1e300;
+    for (int G = 1; G <= ntn; ++G) {
+        const double c = abytes * ((ntn + G - 1) / G) + wbytes * ntm * G / 32.0;
+        if (c < bc) { bc = c; best = G; }
     }
-    constexpr int STAGE = 2 * GB * PBK;  // halfs per stage
-    auto stage = [&](int buf, int k0) {
-        h16* base = smem + buf * STAGE;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int piece = i * 8 + wave;
-            __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + k0), (OSW_LDS void*)(base + piece * 16 * PBK),
-                                             16, 0, 0);
-            __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + k0),
-                                             (OSW_LDS void*)(base + GB * PBK + piece * 16 * PBK), 16, 0, 0);
-        }
-    };
-    const int wm = wave >> 2, wn = wave & 3;
-    f32x4 acc[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    const int nk = g.K / PBK;
-#pragma unroll
-    for (int t = 0; t < PST - 1; ++t)
-        if (t < nk) stage(t, t * PBK);
-    // tile 0 landed: every later tile issued so far may stay in flight
-    if (nk >= 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (nk == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    const int c = lane >> 4;
-    for (int kt = 0; kt < nk; ++kt) {
-        if (kt + PST - 1 < nk) stage((kt + PST - 1) % PST, (kt + PST - 1) * PBK);
-        const h16* la = smem + (kt % PST) * STAGE;
-        const h16* lw = la + GB * PBK;
-        h16x8 b[4];
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-            const int row = wn * 64 + ni * 16 + (lane & 15);
-            b[ni] = *(const h16x8*)&lw[row * PBK + swz32(row, c) * 8];
-        }
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi) {
-            const int row = wm * 128 + mi * 16 + (lane & 15);
-            const h16x8 a = *(const h16x8*)&la[row * PBK + swz32(row, c) * 8];
-#pragma unroll
-            for (int ni = 0; ni < 4; ++ni)
-                acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[ni], acc[mi][ni], 0, 0, 0);
-        }
-        // tile kt+1 must have landed; tiles kt+2, kt+3 (4 glds each per wave) may stay in flight
-        const int ahead = min(nk - 1 - (kt + 1), PST - 2);
-        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-    }
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int m = m0 + wm * 128 + mi * 16 + (lane >> 4) * 4 + i;
-            if (m >= g.M) continue;
-#pragma unroll
-            for (int ni = 0; ni < 4; ++ni) {
-                const int n = n0 + wn * 64 + ni * 16 + (lane & 15);
-                if (n < g.N) store_one<EPI>(g, m, n, acc[mi][ni][i]);
-            }
-        }
+    return best;
 }
 
 template <int EPI>
-void launch256p(const GemmArgs& g, hipStream_t s) {
-    static bool attr = false;
-    constexpr int lds = PST * 2 * GB * PBK * 2;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gemm256p_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        attr = true;
-    }
-    const int nwg = ((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
-    gemm256p_kernel<EPI><<<nwg, GNT, lds, s>>>(g);
-}
-
-template <int EPI>
-void launch256(const GemmArgs& g, hipStream_t s) {
+void launch256(const GemmArgs& g0, hipStream_t s) {
     static bool attr = false;
     constexpr int lds = EPI_LDS > 2 * 2 * GB * BK * 2 ? EPI_LDS : 2 * 2 * GB * BK * 2;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         attr = true;
     }
+    GemmArgs g = g0;
+    g.band = choose_band(g);
     const int nwg = ((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
     gemm256_kernel<EPI><<<nwg, GNT, lds, s>>>(g);
 }
+
+// 8-phase ping-pong variant (cdna_hip_programming.md §5 "The 256² 8-phase template",
+// T3-T5).  Same 256x256x64 tile and 8 waves, but the K-tile is split into four
+// phases of 16 MFMAs (one 64x32 quadrant of the wave's output each), separated by
+// raw s_barriers, and the two 4-wave groups (wm = 0 / 1) run one barrier apart: in
+// every barrier interval one group is in its MFMA cluster while the other issues
+// its ds_reads and global_load_lds, so each SIMD's matrix pipe alternates between
+// its two waves instead of idling through a shared load/wait step.
+//
+// Wave (wm, wn) owns rows {0,128} + wm*64 + [0,64) and cols {0,128} + wn*32 + [0,32),
+// so quadrant (a, b) reads only half-tile A_a (A rows a*128..) and W_b.  LDS holds
+// 2 buffers x 4 half-tiles {A0, A1, W0, W1} x 16 KiB.  Per K-tile t the phases
+// read:  1: A0 + W0   2: W1   3: A1   4: W0 (A1 kept in registers).
+// Every half-tile slot is restaged as soon as it is 2 phases past its last read:
+//   phase 1 stages A1(t+1), 2: W0(t+1), 3: A0(t+2), 4: W1(t+2)
+// and phase 4 waits vmcnt(4) (A0(t+2), W1(t+2) stay in flight), which retires all
+// of tile t+1 one phase before its first read.  The global_load_lds stream is never
+// drained inside the loop (raw s_barrier, no __syncthreads).
+constexpr int HT = 128 * BK;  // halfs per half-tile
+
+template <int EPI>
+__global__ __launch_bounds__(GNT, 1) void gemm8p_kernel(GemmArgs g) {
+    extern __shared__ __attribute__((aligned(16))) h16 smem[];  // [2][A0 A1 W0 W1][128*64]
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int ntn = (g.N + GB - 1) / GB, ntm = (g.M + GB - 1) / GB;
+    const int nwg = ntn * ntm;
+    const int bid = blockIdx.x;
+    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+    const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+    const int G = g.band > 0 ? min(g.band, ntn) : ntn;
+    const int band = tile / (G * ntm), rr0 = tile % (G * ntm);
+    const int gw = min(G, ntn - band * G);
+    const int n0 = (band * G + rr0 % gw) * GB, m0 = (rr0 / gw) * GB;
+
+    // glds sources: half-tile H, piece i*8 + wave (8 rows of 128 B), lane -> row, swizzled chunk
+    const h16* src[4][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int rr = (i * 8 + wave) * 8 + (lane >> 3);
+        const int c = swz(rr, lane & 7);
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            src[hh][i] = grp_row(g.A, min(m0 + hh * 128 + rr, g.M - 1), g.a_grp_rows, g.a_grp_stride, g.lda) + c * 8;
+            src[2 + hh][i] = g.W + (int64_t)min(n0 + hh * 128 + rr, g.N - 1) * g.ldw + c * 8;
+        }
+    }
+    auto stage = [&](int H, int t) {
+        h16* base = smem + ((t & 1) * 4 + H) * HT;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(src[H][i] + t * BK),
+                                             (OSW_LDS void*)(base + (i * 8 + wave) * 8 * BK), 16, 0, 0);
+    };
+    const int wm = wave >> 2, wn = wave & 3;
+    const int li = lane & 15, lc = lane >> 4;
+    // per-lane LDS element offsets of the fragment reads (swizzle is the same for every 16-row step)
+    const int aoff0 = (wm * 64 + li) * BK + swz(wm * 64 + li, lc) * 8;
+    const int aoff1 = (wm * 64 + li) * BK + swz(wm * 64 + li, 4 + lc) * 8;
+    const int boff0 = (wn * 32 + li) * BK + swz(wn * 32 + li, lc) * 8;
+    const int boff1 = (wn * 32 + li) * BK + swz(wn * 32 + li, 4 + lc) * 8;
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    h16x8 af[4][2], bf[2][2];
+
+    auto read_a = [&](const h16* hb) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+            af[mt][0] = *(const h16x8*)&hb[aoff0 + mt * 16 * BK];
+            af[mt][1] = *(const h16x8*)&hb[aoff1 + mt * 16 * BK];
+        }
+    };
+    auto read_b = [&](const h16* hb) {
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+            bf[nt][0] = *(const h16x8*)&hb[boff0 + nt * 16 * BK];
+            bf[nt][1] = *(const h16x8*)&hb[boff1 + nt * 16 * BK];
+        }
+    };
+    auto barrier = [] {
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+    auto mfma = [&](int a, int b) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                f32x4 c = acc[a * 4 + mt][b * 2 + nt];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mt][0], bf[nt][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mt][1], bf[nt][1], c, 0, 0, 0);
+                acc[a * 4 + mt][b * 2 + nt] = c;
+            }
+        __builtin_amdgcn_s_setprio(0);
+    };
+
+    const int nk = g.K / BK;
+    // prologue = phases 3, 4 of tile -2 and tile -1 in the steady-state order
+    stage(0, 0);
+    stage(3, 0);
+    stage(1, 0);
+    stage(2, 0);
+    if (nk > 1) {
+        stage(0, 1);
+        stage(3, 1);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    barrier();
+    if (__builtin_amdgcn_readfirstlane(wave) >= 4) barrier();  // group 1 runs one barrier behind group 0
+
+    for (int t = 0; t < nk; ++t) {
+        const h16* buf = smem + (t & 1) * 4 * HT;
+        const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
+        // phase 1: quadrant (0,0)
+        if (n1) stage(1, t + 1);
+        read_a(buf + 0 * HT);
+        read_b(buf + 2 * HT);
+        barrier();
+        mfma(0, 0);
+        barrier();
+        // phase 2: quadrant (0,1)
+        if (n1) stage(2, t + 1);
+        read_b(buf + 3 * HT);
+        barrier();
+        mfma(0, 1);
+        barrier();
+        // phase 3: quadrant (1,1)
+        if (n2) stage(0, t + 2);
+        read_a(buf + 1 * HT);
+        barrier();
+        mfma(1, 1);
+        barrier();
+        // phase 4: quadrant (1,0); retire tile t+1
+        if (n2) {
+            stage(3, t + 2);
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        read_b(buf + 2 * HT);
+        barrier();
+        mfma(1, 0);
+        barrier();
+    }
+    if (__builtin_amdgcn_readfirstlane(wave) < 4) barrier();
+    staged_epilogue<EPI, true>(g, acc, m0, n0, wm, wn, (char*)smem);
+}
+
+template <int EPI>
+void launch8p(const GemmArgs& g0, hipStream_t s) {
+    static bool attr = false;
+    constexpr int lds = EPI_LDS > 8 * HT * 2 ? EPI_LDS : 8 * HT * 2;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)gemm8p_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        attr = true;
+    }
+    GemmArgs g = g0;
+    g.band = choose_band(g);
+    const int nwg = ((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
+    gemm8p_kernel<EPI><<<nwg, GNT, lds, s>>>(g);
+}
+
 
 // ---------------------------------------------------------------------------
 // Skinny GEMM for the decoder (M <= 64 rows = windows in the batch): weight-
@@ -639,12 +731,12 @@ void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s) {
     const bool big = variant == 2 || (variant == 0 && big_tiles >= 512 && g.N % 8 == 0 && !getenv("OSW_GEMM128"));
     if (variant == 4) {
         switch (g.epi) {
-            case EPI_F16: launch256p<EPI_F16>(g, s); return;
-            case EPI_F16_GELU: launch256p<EPI_F16_GELU>(g, s); return;
-            case EPI_F32_RESID: launch256p<EPI_F32_RESID>(g, s); return;
-            case EPI_F32_GELU_POS: launch256p<EPI_F32_GELU_POS>(g, s); return;
-            case EPI_F32: launch256p<EPI_F32>(g, s); return;
-            default: launch256p<EPI_HEADS>(g, s); return;
+            case EPI_F16: launch8p<EPI_F16>(g, s); return;
+            case EPI_F16_GELU: launch8p<EPI_F16_GELU>(g, s); return;
+            case EPI_F32_RESID: launch8p<EPI_F32_RESID>(g, s); return;
+            case EPI_F32_GELU_POS: launch8p<EPI_F32_GELU_POS>(g, s); return;
+            case EPI_F32: launch8p<EPI_F32>(g, s); return;
+            default: launch8p<EPI_HEADS>(g, s); return;
         }
     }
     if (big) {

@@ -729,7 +729,8 @@ void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s) {
     // big tile when it still yields >= 2 waves of workgroups over 256 CUs
     const int64_t big_tiles = (int64_t)((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
     const bool big = variant == 2 || (variant == 0 && big_tiles >= 512 && g.N % 8 == 0 && !getenv("OSW_GEMM128"));
-    if (variant == 4) {
+    static const bool two_phase = getenv("OSW_GEMM_2PHASE") != nullptr;  // A/B switch for the 8-phase schedule
+    if (variant == 4 || (variant == 0 && big && !two_phase)) {
         switch (g.epi) {
             case EPI_F16: launch8p<EPI_F16>(g, s); return;
             case EPI_F16_GELU: launch8p<EPI_F16_GELU>(g, s); return;

@@ -14,6 +14,7 @@ from open_speech_amd import dims as D  # noqa: E402
 from open_speech_amd.engine import WhisperEngine  # noqa: E402
 
 SHAPES = [  # name, M, N, K, variants
+    ("sq4096", 4096, 4096, 4096, (2, 4)), ("sq8192", 8192, 8192, 8192, (2, 4)),
     ("enc_qkv", 96000, 3840, 1280, (1, 2, 4)), ("enc_o", 96000, 1280, 1280, (1, 2, 4)),
     ("enc_fc1", 96000, 5120, 1280, (1, 2, 4)), ("enc_fc2", 96000, 1280, 5120, (1, 2, 4)),
     ("dec_qkv", 64, 3840, 1280, (3,)), ("dec_fc2", 64, 1280, 5120, (3,)), ("dec_o", 64, 1280, 1280, (3,)),

@@ -73,6 +73,13 @@ typedef struct osw_decode_opts {
     /* optional per-window language tokens (n_windows ints; -1 = detect); NULL: use
      * language_token for every window */
     const int32_t* language_tokens;
+    /* beam search (CTranslate2 BeamSearch semantics, as faster-whisper calls it):
+     * beam_size <= 1 is greedy; windows * beam_size <= 5 * max_batch.  A caller
+     * that sets beam_size > 1 must set length_penalty (0 = no length normalisation). */
+    int32_t beam_size;           /* reference default 5 (src/backends/faster_whisper.py:237) */
+    float patience;              /* <= 0 -> 1; stop once round(beam*patience) hypotheses finished */
+    float length_penalty;        /* score / len**length_penalty ranks finished hypotheses */
+    int32_t num_hypotheses;      /* <= 0 -> 1 */
 } osw_decode_opts;
 
 /* Caller-allocated outputs for n windows. */

@@ -32,7 +32,9 @@ class osw_decode_opts(C.Structure):
                 ("no_timestamps", C.c_int32), ("timestamp_begin", C.c_int32), ("blank", C.c_int32),
                 ("first_lang", C.c_int32), ("n_langs", C.c_int32),
                 ("prefix_tokens", C.POINTER(C.c_int32)), ("n_prefix", C.c_int32),
-                ("language_tokens", C.POINTER(C.c_int32))]
+                ("language_tokens", C.POINTER(C.c_int32)),
+                ("beam_size", C.c_int32), ("patience", C.c_float), ("length_penalty", C.c_float),
+                ("num_hypotheses", C.c_int32)]
 
 
 class osw_window_result(C.Structure):

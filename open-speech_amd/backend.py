@@ -12,9 +12,10 @@ Kept exactly: ``_models`` / ``_loaded_at`` / ``_last_used`` dicts (read by
 ``src/lifecycle.py:46-73``), idempotent ``load_model``, auto-load on first use,
 ``_last_used`` refresh per call, return shapes per ``response_format``, exceptions
 propagated to the caller (HTTP 500 / WS error / Wyoming "").
-Differences by design: audio bytes are parsed in memory (no temp file, no PyAV),
-decoding is greedy (``beam_size=1``; the reference's beam 5 is the next §8(f) row),
-and concurrent calls are batched on the GPU behind the blocking ``transcribe``.
+Decoding is beam search width 5 like the reference (``STT_HIP_BEAM_SIZE=1`` selects
+greedy, the parity mode).  Differences by design: audio bytes are parsed in memory
+(no temp file, no PyAV) and concurrent calls are batched on the GPU behind the
+blocking ``transcribe``.
 """
 from __future__ import annotations
 
@@ -214,7 +215,8 @@ class HipWhisperBackend:
         m = self._ensure_model(model_id)
         pcm = decode_audio_bytes(audio)
         opts = TranscribeOptions(task=task, language=language if (language and task == "transcribe") else None,
-                                 initial_prompt=prompt or None, temperature=float(temperature or 0.0))
+                                 initial_prompt=prompt or None, temperature=float(temperature or 0.0),
+                                 beam_size=int(os.environ.get("STT_HIP_BEAM_SIZE", "5")))
         res = m.runner.transcribe(pcm, opts)
         return shape_response(task, res, response_format)
 

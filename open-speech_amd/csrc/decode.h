@@ -1,0 +1,46 @@
+// Decoder-side state shared by decode.hip (kernels) and osw.hip (host pipeline).
+#pragma once
+#include "common.h"
+
+namespace osw {
+
+// Per decoder row (a window, or one beam hypothesis of a window).  Lives in device
+// memory so a step needs no host round trip.
+struct SelState {
+    int n_sampled, last, penult, last_ts, done, lang;
+    float sum_lp, nsp;  // greedy: Σ log-prob of the picks; beam: the hypothesis' cumulative score
+};
+
+struct SelParams {
+    int prompt_len;        // P: positions 0..P-1 are prompt
+    int sot_pos;           // position of <|startoftranscript|> in the prompt
+    int lang_pos;          // prompt position holding the language token (-1 placeholder => detect)
+    int max_length;
+    int V, eot, no_speech, no_ts, tb, blank, first_lang, n_langs;
+    int suppress_blank, with_ts, max_init_ts;
+    int beam;              // hypotheses per window (1 = greedy)
+    int num_hyp, max_cand; // beam stop rule: num_hypotheses, round(beam * patience)
+    float length_penalty;
+};
+
+// Per window in beam mode: finished-hypothesis bookkeeping (the best one's tokens
+// are copied to a per-window buffer when it improves).
+struct BeamWin {
+    int n_hyp, best_len, done, pad;
+    float best_norm, best_raw;
+};
+
+constexpr int MAX_BEAM = 8;
+constexpr int SEL_SPLIT = 16;  // vocabulary slices per row in the selection kernels
+
+void launch_select(const float* logits, int rows, const int* pos, const SelParams& P, const int* prompt,
+                   const unsigned* supmask, SelState* st, int* cur_tok, int* tokens, int max_tokens, void* sel_parts,
+                   hipStream_t s);
+void launch_beam(const float* logits, int windows, const int* pos, const SelParams& P, const unsigned* supmask,
+                 SelState* st, const void* sel_parts, void* cand, int* seq, int* anc, int ctx, BeamWin* bw,
+                 int* best_tok, int* cur_tok, int max_tokens, hipStream_t s);
+int sel_parts_bytes();
+int beam_cand_bytes(int beam);
+void launch_count_done(const SelState* st, int rows, int* out, hipStream_t s);
+
+}  // namespace osw

@@ -6,7 +6,9 @@
 // K and V of every (window, head): 2 x 1500 x 64 fp16 = 384 KB per (b, h).  One
 // workgroup per (b, h); K rows are read 128 B per lane (8 x 16 B), V in 1 KiB
 // contiguous wave-instructions (8 rows x 128 B), scores stay in LDS.
-#include "common.h"
+#include "decode.h"
+
+#include <climits>
 
 namespace osw {
 
@@ -38,16 +40,29 @@ __device__ __forceinline__ float block_reduce_sum(float v, float* red) {
 // 256 threads.  Scores live in LDS (n_keys <= MAXK).  Loads are issued in groups
 // (2 K rows = 16 x 16 B per lane, 8 V pieces per lane) before the FMAs that use
 // them so each lane keeps several HBM requests in flight.
-template <int MAXK>
+//
+// GATHER (beam search): key p of this row lives in the cache slot of the row that
+// wrote position p of this hypothesis' history: K + soff[p] * slot_stride, where
+// soff[p] = anc[p] - self (staged in LDS; the newest key is always this row's own).
+template <int MAXK, bool GATHER = false>
 __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ K, const h16* __restrict__ V,
-                           int n_keys, h16* __restrict__ out) {
+                           int n_keys, h16* __restrict__ out, const int* __restrict__ anc = nullptr, int self = 0,
+                           int64_t slot_stride = 0) {
     __shared__ float qs[HD];
     __shared__ float sc[MAXK];
     __shared__ float red[8];
     __shared__ f32x4 part[32][17];  // [key group][8 d-chunks x 2 float4]
+    __shared__ int soff[GATHER ? MAXK : 1];
     const int tid = threadIdx.x;
     if (tid < HD) qs[tid] = (float)q16[tid] * 0.125f;  // 1/sqrt(64), exact in fp32
+    if constexpr (GATHER) {
+        for (int p = tid; p < n_keys; p += 256) soff[p] = p + 1 < n_keys ? anc[p] - self : 0;
+    }
     __syncthreads();
+    auto krow = [&](const h16* base, int key) -> const h16* {
+        if constexpr (GATHER) return base + (int64_t)soff[key] * slot_stride + (int64_t)key * HD;
+        return base + (int64_t)key * HD;
+    };
     // scores: 8 lanes per key row (lane c holds dims 8c..8c+7), so one wave-instruction
     // reads 8 consecutive K rows = 1 KiB contiguous; 4 such loads in flight per lane;
     // the 8-lane partial dots are combined with 3 xor-shuffles.
@@ -61,7 +76,7 @@ __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ 
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int key = min(base + u * 32 + w * 8 + kr, n_keys - 1);
-            kv[u] = *(const h16x8*)(K + (int64_t)key * HD + 8 * c8);
+            kv[u] = *(const h16x8*)(krow(K, key) + 8 * c8);
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -95,7 +110,7 @@ __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ 
         h16x8 v[8];
         float p[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = *(const h16x8*)(V + (int64_t)(j + 32 * u) * HD + 8 * c);
+        for (int u = 0; u < 8; ++u) v[u] = *(const h16x8*)(krow(V, j + 32 * u) + 8 * c);
 #pragma unroll
         for (int u = 0; u < 8; ++u) p[u] = sc[j + 32 * u];
 #pragma unroll
@@ -104,7 +119,7 @@ __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ 
             for (int e = 0; e < 8; ++e) acc[e] = fmaf(p[u], (float)v[u][e], acc[e]);
     }
     for (; j < n_keys; j += 32) {
-        const h16x8 v = *(const h16x8*)(V + (int64_t)j * HD + 8 * c);
+        const h16x8 v = *(const h16x8*)(krow(V, j) + 8 * c);
         const float p = sc[j];
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[e] = fmaf(p, (float)v[e], acc[e]);
@@ -146,7 +161,8 @@ __device__ __forceinline__ void reduce_head(const float* __restrict__ part, int 
 __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restrict__ part, int ks,
                                                             const float* __restrict__ bias, h16* __restrict__ kcache,
                                                             h16* __restrict__ vcache, const int* __restrict__ pos_ptr,
-                                                            int H, int B, int ctx, h16* __restrict__ out) {
+                                                            int H, int B, int ctx, h16* __restrict__ out,
+                                                            const int* __restrict__ anc) {
     __shared__ h16 q16[HD];
     __shared__ float red4[256];
     const int h = blockIdx.x, b = blockIdx.y;
@@ -160,21 +176,31 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
     reduce_head(part, ks, slab, row + 2 * D + h * HD, bias, 2 * D + h * HD, vc + (int64_t)pos * HD, red4);
     __threadfence_block();
     __syncthreads();
-    attend_one<448>(q16, kc, vc, pos + 1, out + (int64_t)b * D + h * HD);
+    if (anc)
+        attend_one<448, true>(q16, kc, vc, pos + 1, out + (int64_t)b * D + h * HD, anc + (int64_t)b * ctx, b,
+                              (int64_t)H * ctx * HD);
+    else
+        attend_one<448>(q16, kc, vc, pos + 1, out + (int64_t)b * D + h * HD);
 }
 
-// grid (H, B): q = Σ split-K partials of the cross-attention q projection + bias;
-// xkv layer slice: K at ((b*H + h)*T*64) of xk, V likewise of xv
+// grid H*B (flattened): q = Σ split-K partials of the cross-attention q projection
+// + bias; row b attends window b / beam: K at ((w*H + h)*T*64) of xk, V likewise.
+// Workgroups are remapped XCD-contiguously with the beam rows of one (window, head)
+// adjacent, so those rows' reads of the same 384 KB K/V share one L2.
 __global__ __launch_bounds__(256) void dec_cross_attn_kernel(const float* __restrict__ part, int ks,
                                                              const float* __restrict__ bias,
                                                              const h16* __restrict__ xk, const h16* __restrict__ xv,
-                                                             int H, int B, int T, h16* __restrict__ out) {
+                                                             int H, int B, int T, int beam, h16* __restrict__ out) {
     __shared__ h16 q16[HD];
     __shared__ float red4[256];
-    const int h = blockIdx.x, b = blockIdx.y;
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int qq = nwg / 8, rr = nwg % 8, xcd = bid % 8;
+    const int lin = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + bid / 8;
+    const int k = lin % beam, h = (lin / beam) % H, w = lin / (beam * H);
+    const int b = w * beam + k;
     const int D = H * HD;
     reduce_head(part, ks, (int64_t)B * D, (int64_t)b * D + h * HD, bias, h * HD, q16, red4);
-    const int64_t hoff = ((int64_t)b * H + h) * T * HD;
+    const int64_t hoff = ((int64_t)w * H + h) * T * HD;
     attend_one<1536>(q16, xk + hoff, xv + hoff, T, out + (int64_t)b * D + h * HD);
 }
 
@@ -253,20 +279,6 @@ __global__ __launch_bounds__(256) void dec_reduce_gelu_kernel(const float* __res
 // ---------------------------------------------------------------------------
 // Greedy selection.  Per-window state lives in device memory so a step needs no
 // host round trip.
-struct SelState {
-    int n_sampled, last, penult, last_ts, done, lang;
-    float sum_lp, nsp;
-};
-
-struct SelParams {
-    int prompt_len;        // P: positions 0..P-1 are prompt
-    int sot_pos;           // position of <|startoftranscript|> in the prompt
-    int lang_pos;          // prompt position holding the language token (-1 placeholder => detect)
-    int max_length;
-    int V, eot, no_speech, no_ts, tb, blank, first_lang, n_langs;
-    int suppress_blank, with_ts, max_init_ts;
-};
-
 struct ArgMax {
     float v;
     int i;
@@ -302,13 +314,45 @@ struct SelPart {
     float v_all, v_text, v_ts;
     int i_all, i_text, i_ts;
 };
-constexpr int SEL_SPLIT = 16;
 
 enum { SEL_PROMPT = 0, SEL_SOT = 1, SEL_SAMPLE = 2, SEL_DONE = 3 };
 
 __device__ __forceinline__ int sel_mode(const SelParams& P, int step, const SelState& s) {
     if (step < P.prompt_len - 1) return step == P.sot_pos ? SEL_SOT : SEL_PROMPT;
     return s.done ? SEL_DONE : SEL_SAMPLE;
+}
+
+// The logits rules for one row at its current state (SuppressBlank, SuppressTokens,
+// ApplyTimestampRules without the mass rule, which needs the slice statistics).
+struct RowRules {
+    int n, ts_block;
+    bool last_ts, pen_ts;
+};
+__device__ __forceinline__ RowRules row_rules(const SelParams& P, const SelState& s) {
+    RowRules R;
+    R.n = s.n_sampled;
+    R.last_ts = R.n >= 1 && s.last >= P.tb;
+    R.pen_ts = R.n < 2 || s.penult >= P.tb;
+    R.ts_block = P.tb;  // timestamps in [tb, ts_block) are forbidden (monotonicity)
+    if (P.with_ts && s.last_ts > 0) R.ts_block = (R.last_ts && !R.pen_ts) ? s.last_ts : s.last_ts + 1;
+    return R;
+}
+__device__ __forceinline__ bool tok_masked(const SelParams& P, const RowRules& R, const unsigned* supmask, int v) {
+    bool masked = (supmask[v >> 5] >> (v & 31)) & 1u;
+    if (P.suppress_blank && R.n == 0 && (v == P.blank || v == P.eot)) masked = true;
+    if (P.with_ts) {
+        if (v == P.no_ts) masked = true;
+        if (R.last_ts) {
+            if (R.pen_ts) { if (v >= P.tb) masked = true; }
+            else { if (v < P.eot) masked = true; }
+        }
+        if (v >= P.tb && v < R.ts_block) masked = true;
+        if (R.n == 0) {
+            if (v < P.tb) masked = true;
+            if (P.max_init_ts >= 0 && v > P.tb + P.max_init_ts) masked = true;
+        }
+    }
+    return masked;
 }
 
 // grid (B, SEL_SPLIT), 256 threads
@@ -325,11 +369,7 @@ __global__ __launch_bounds__(256) void select_partial_kernel(const float* __rest
     const float* x = logits + (int64_t)b * P.V;
     const int per = (P.V + SEL_SPLIT - 1) / SEL_SPLIT;
     const int lo = sl * per, hi = min(P.V, lo + per);
-    const int n = s.n_sampled;
-    const bool last_ts = n >= 1 && s.last >= P.tb;
-    const bool pen_ts = n < 2 || s.penult >= P.tb;
-    int ts_block = P.tb;  // timestamps in [tb, ts_block) are forbidden (monotonicity)
-    if (P.with_ts && s.last_ts > 0) ts_block = (last_ts && !pen_ts) ? s.last_ts : s.last_ts + 1;
+    const RowRules R = row_rules(P, s);
     float m_all = -INFINITY, s_all = 0.f, m_ts = -INFINITY, s_ts = 0.f;
     ArgMax a_all{-INFINITY, 0x7fffffff}, a_text{-INFINITY, 0x7fffffff}, a_ts{-INFINITY, 0x7fffffff};
     for (int v = lo + tid; v < hi; v += 256) {
@@ -339,21 +379,7 @@ __global__ __launch_bounds__(256) void select_partial_kernel(const float* __rest
             if (v >= P.first_lang && v < P.first_lang + P.n_langs) a_text = amax(a_text, ArgMax{xv, v});
             continue;
         }
-        bool masked = (supmask[v >> 5] >> (v & 31)) & 1u;
-        if (P.suppress_blank && n == 0 && (v == P.blank || v == P.eot)) masked = true;
-        if (P.with_ts) {
-            if (v == P.no_ts) masked = true;
-            if (last_ts) {
-                if (pen_ts) { if (v >= P.tb) masked = true; }
-                else { if (v < P.eot) masked = true; }
-            }
-            if (v >= P.tb && v < ts_block) masked = true;
-            if (n == 0) {
-                if (v < P.tb) masked = true;
-                if (P.max_init_ts >= 0 && v > P.tb + P.max_init_ts) masked = true;
-            }
-        }
-        if (masked) continue;
+        if (tok_masked(P, R, supmask, v)) continue;
         lse_add(m_all, s_all, xv);
         a_all = amax(a_all, ArgMax{xv, v});
         if (v >= P.tb) {
@@ -392,6 +418,20 @@ __global__ __launch_bounds__(256) void select_partial_kernel(const float* __rest
     }
 }
 
+__device__ SelPart combine_parts(const SelPart* __restrict__ parts) {
+    SelPart r = parts[0];
+    for (int i = 1; i < SEL_SPLIT; ++i) {
+        const SelPart& q = parts[i];
+        lse_merge(r.m_all, r.s_all, q.m_all, q.s_all);
+        lse_merge(r.m_ts, r.s_ts, q.m_ts, q.s_ts);
+        ArgMax A = amax(ArgMax{r.v_all, r.i_all}, ArgMax{q.v_all, q.i_all});
+        ArgMax X = amax(ArgMax{r.v_text, r.i_text}, ArgMax{q.v_text, q.i_text});
+        ArgMax T = amax(ArgMax{r.v_ts, r.i_ts}, ArgMax{q.v_ts, q.i_ts});
+        r.v_all = A.v; r.i_all = A.i; r.v_text = X.v; r.i_text = X.i; r.v_ts = T.v; r.i_ts = T.i;
+    }
+    return r;
+}
+
 // grid B, 64 threads: combine the slices in fixed order, apply the timestamp-mass
 // rule, pick the token, update the window state.
 __global__ __launch_bounds__(64) void select_final_kernel(const float* __restrict__ logits, SelParams P,
@@ -414,16 +454,8 @@ __global__ __launch_bounds__(64) void select_final_kernel(const float* __restric
         cur_tok[b] = P.eot;
         return;
     }
-    SelPart r = parts[b * SEL_SPLIT];
-    for (int i = 1; i < SEL_SPLIT; ++i) {
-        const SelPart& q = parts[b * SEL_SPLIT + i];
-        lse_merge(r.m_all, r.s_all, q.m_all, q.s_all);
-        lse_merge(r.m_ts, r.s_ts, q.m_ts, q.s_ts);
-        ArgMax A = amax(ArgMax{r.v_all, r.i_all}, ArgMax{q.v_all, q.i_all});
-        ArgMax X = amax(ArgMax{r.v_text, r.i_text}, ArgMax{q.v_text, q.i_text});
-        ArgMax T = amax(ArgMax{r.v_ts, r.i_ts}, ArgMax{q.v_ts, q.i_ts});
-        r.v_all = A.v; r.i_all = A.i; r.v_text = X.v; r.i_text = X.i; r.v_ts = T.v; r.i_ts = T.i;
-    }
+    if (mode == SEL_SAMPLE && P.beam > 1) return;  // beam rows: beam_topk / beam_update
+    const SelPart r = combine_parts(parts + b * SEL_SPLIT);
     const float lse_all = r.m_all + __logf(r.s_all);
     if (mode == SEL_SOT) {
         const float* x = logits + (int64_t)b * P.V;
@@ -460,6 +492,217 @@ __global__ __launch_bounds__(64) void select_final_kernel(const float* __restric
     cur_tok[b] = next;
 }
 
+// ---------------------------------------------------------------------------
+// Beam search (restated CTranslate2 BeamSearch, see oracle/decode.py): per row the
+// processed log-probs (rules + log-softmax, timestamp-mass rule) plus the row's
+// cumulative score; per window the top 2*beam candidates over beam x vocab, the
+// finished-hypothesis bookkeeping and the reorder of the surviving hypotheses.
+// The KV cache is never copied: row r's key at position p lives in the slot of row
+// anc[r][p] (written at step p); the reorder copies only anc / tokens / state.
+struct BeamCand {
+    float s;
+    int i;  // flat index within the window: beam slot * V + token
+};
+
+// block-wide argmax (value desc, index asc) of one candidate per thread, 256 threads
+__device__ __forceinline__ ArgMax block_amax(ArgMax a, ArgMax* red) {
+    for (int o = 32; o > 0; o >>= 1) a = amax(a, ArgMax{__shfl_xor(a.v, o, 64), __shfl_xor(a.i, o, 64)});
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = a;
+    __syncthreads();
+    ArgMax r = red[0];
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) r = amax(r, red[i]);
+    return r;
+}
+
+constexpr int BEAM_SLICE = 4096;  // >= ceil(V / SEL_SPLIT) for V <= 65536
+
+// grid (rows, SEL_SPLIT), 256 threads: top 2*beam (score, flat) of one vocabulary slice
+__global__ __launch_bounds__(256) void beam_topk_kernel(const float* __restrict__ logits, SelParams P,
+                                                        const int* __restrict__ pos_ptr,
+                                                        const unsigned* __restrict__ supmask,
+                                                        const SelState* __restrict__ st,
+                                                        const SelPart* __restrict__ parts, BeamCand* __restrict__ cand) {
+    __shared__ float sc[BEAM_SLICE];
+    __shared__ float stat[3];
+    __shared__ ArgMax red[4];
+    const int row = blockIdx.x, sl = blockIdx.y, tid = threadIdx.x;
+    const int step = *pos_ptr;
+    const SelState s = st[row];
+    if (sel_mode(P, step, s) != SEL_SAMPLE) return;
+    const int K2 = 2 * P.beam, k = row % P.beam;
+    BeamCand* out = cand + ((int64_t)row * SEL_SPLIT + sl) * K2;
+    if (step == P.prompt_len - 1 && k != 0) {  // first sampled step: only the prompt hypothesis expands
+        if (tid < K2) out[tid] = BeamCand{-INFINITY, INT_MAX};
+        return;
+    }
+    if (tid == 0) {
+        const SelPart r = combine_parts(parts + (int64_t)row * SEL_SPLIT);
+        const float lse_all = r.m_all + logf(r.s_all);
+        const float lse_ts = r.m_ts == -INFINITY ? -INFINITY : r.m_ts + logf(r.s_ts);
+        stat[0] = lse_all;
+        stat[1] = lse_ts;
+        stat[2] = (P.with_ts && lse_ts - lse_all > r.v_text - lse_all) ? 1.f : 0.f;
+    }
+    __syncthreads();
+    const float lse_all = stat[0], lse_ts = stat[1];
+    const bool ts_wins = stat[2] != 0.f;
+    const RowRules R = row_rules(P, s);
+    const int per = (P.V + SEL_SPLIT - 1) / SEL_SPLIT;
+    const int lo = sl * per, hi = min(P.V, lo + per);
+    const float* x = logits + (int64_t)row * P.V;
+    for (int v = lo + tid; v < hi; v += 256) {
+        float lp = -INFINITY;
+        if (!tok_masked(P, R, supmask, v)) {
+            if (!ts_wins) lp = x[v] - lse_all;
+            else if (v >= P.tb) lp = x[v] - lse_ts;
+        }
+        sc[v - lo] = s.sum_lp + lp;
+    }
+    __syncthreads();
+    const int base = k * P.V + lo;
+    for (int r = 0; r < K2; ++r) {
+        ArgMax a{-INFINITY, INT_MAX};
+        for (int i = tid; i < hi - lo; i += 256) a = amax(a, ArgMax{sc[i], base + i});  // NaN = taken
+        a = block_amax(a, red);
+        if (tid == 0) {
+            out[r] = BeamCand{a.v, a.i};
+            if (a.i != INT_MAX) sc[a.i - base] = __builtin_nanf("");
+        }
+        __syncthreads();
+    }
+}
+
+// grid windows, 256 threads: merge the candidates, register finished hypotheses,
+// pick the surviving beams and reorder their tokens / ancestry / state.
+__global__ __launch_bounds__(256) void beam_update_kernel(SelParams P, const int* __restrict__ pos_ptr,
+                                                          SelState* __restrict__ st,
+                                                          const BeamCand* __restrict__ cand, int* __restrict__ seq,
+                                                          int* __restrict__ anc, int ctx, BeamWin* __restrict__ bwin,
+                                                          int* __restrict__ best_tok, int* __restrict__ cur_tok,
+                                                          int max_tokens) {
+    constexpr int MAXC = MAX_BEAM * SEL_SPLIT * 2 * MAX_BEAM;
+    __shared__ float cs[MAXC];
+    __shared__ int ci[MAXC];
+    __shared__ BeamCand top[2 * MAX_BEAM];
+    __shared__ ArgMax red[4];
+    __shared__ int lseq[MAX_BEAM][448];
+    __shared__ int lanc[MAX_BEAM][448];
+    __shared__ SelState lst[MAX_BEAM];
+    __shared__ int choose[MAX_BEAM], fin, best_src, best_extra, improved;
+    const int w = blockIdx.x, tid = threadIdx.x, K = P.beam, K2 = 2 * K;
+    const int r0 = w * K;
+    const int step = *pos_ptr;
+    if (sel_mode(P, step, st[r0]) != SEL_SAMPLE) return;
+    const int nc = K * SEL_SPLIT * K2;
+    for (int i = tid; i < nc; i += 256) {
+        const BeamCand c = cand[(int64_t)r0 * SEL_SPLIT * K2 + i];
+        cs[i] = c.s;
+        ci[i] = c.i;
+    }
+    const int n = st[r0].n_sampled;  // identical for every row of the window
+    for (int i = tid; i < K * max(n, 1); i += 256) {
+        const int k = i / max(n, 1), j = i % max(n, 1);
+        if (j < n) lseq[k][j] = seq[(int64_t)(r0 + k) * max_tokens + j];
+    }
+    for (int i = tid; i < K * step; i += 256) {
+        const int k = i / step, p = i % step;
+        lanc[k][p] = anc[(int64_t)(r0 + k) * ctx + p];
+    }
+    if (tid < K) lst[tid] = st[r0 + tid];
+    __syncthreads();
+    for (int r = 0; r < K2; ++r) {
+        ArgMax a{-INFINITY, INT_MAX};
+        int at = -1;
+        for (int i = tid; i < nc; i += 256) {
+            const ArgMax b{cs[i], ci[i]};
+            if (b.i != INT_MAX && !(b.v != b.v)) {
+                const ArgMax m = amax(a, b);
+                if (m.i != a.i || m.v != a.v) { a = m; at = i; }
+            }
+        }
+        const ArgMax g = block_amax(a, red);
+        if (a.i == g.i && at >= 0 && g.i != INT_MAX) cs[at] = __builtin_nanf("");  // unique flat ids: one owner
+        if (tid == 0) top[r] = BeamCand{g.v, g.i};
+        __syncthreads();
+    }
+    if (tid == 0) {
+        BeamWin bw = bwin[w];
+        const bool is_last = P.prompt_len + n + 1 >= P.max_length;
+        int sec = K;
+        bool top_fin = false;
+        improved = 0;
+        for (int k = 0; k < K; ++k) {
+            const BeamCand c = top[k];
+            const int tok = c.i == INT_MAX ? P.eot : c.i % P.V;
+            int nb = k;
+            if (tok == P.eot || is_last) {
+                if (k == 0) top_fin = true;
+                const int len = n + (tok == P.eot ? 0 : 1);
+                const float norm = len == 0 ? (P.length_penalty != 0.f ? -INFINITY : c.s)
+                                            : c.s / powf((float)len, P.length_penalty);
+                bw.n_hyp += 1;
+                if (bw.n_hyp == 1 || norm > bw.best_norm) {
+                    bw.best_norm = norm;
+                    bw.best_raw = c.s;
+                    bw.best_len = min(len, max_tokens);
+                    best_src = c.i == INT_MAX ? 0 : c.i / P.V;
+                    best_extra = tok == P.eot ? -1 : tok;
+                    improved = 1;
+                }
+                for (int j = sec; j < K2; ++j) {
+                    const int t2 = top[j].i == INT_MAX ? P.eot : top[j].i % P.V;
+                    if (t2 != P.eot) {
+                        nb = j;
+                        sec = j + 1;
+                        break;
+                    }
+                }
+            }
+            choose[k] = nb;
+        }
+        fin = is_last || (top_fin && bw.n_hyp >= P.num_hyp) || bw.n_hyp >= P.max_cand;
+        bw.done = fin;
+        bwin[w] = bw;
+    }
+    __syncthreads();
+    if (improved) {
+        int* dst = best_tok + (int64_t)w * max_tokens;
+        for (int j = tid; j < n && j < max_tokens; j += 256) dst[j] = lseq[best_src][j];
+        if (tid == 0 && best_extra >= 0 && n < max_tokens) dst[n] = best_extra;
+    }
+    if (fin) {
+        if (tid < K) {
+            SelState s2 = lst[tid];
+            s2.done = 1;
+            st[r0 + tid] = s2;
+            cur_tok[r0 + tid] = P.eot;
+        }
+        return;
+    }
+    for (int k = 0; k < K; ++k) {
+        const BeamCand c = top[choose[k]];
+        const int q = c.i == INT_MAX ? 0 : c.i / P.V;
+        const int tok = c.i == INT_MAX ? P.eot : c.i % P.V;
+        int* sq = seq + (int64_t)(r0 + k) * max_tokens;
+        for (int j = tid; j < n && j < max_tokens; j += 256) sq[j] = lseq[q][j];
+        int* an = anc + (int64_t)(r0 + k) * ctx;
+        for (int p = tid; p <= step && p < ctx; p += 256) an[p] = p < step ? lanc[q][p] : r0 + q;
+        if (tid == 0) {
+            if (n < max_tokens) sq[n] = tok;
+            SelState s2 = lst[q];
+            s2.n_sampled = n + 1;
+            s2.penult = s2.last;
+            s2.last = tok;
+            if (tok >= P.tb) s2.last_ts = tok;
+            s2.sum_lp = c.s;
+            st[r0 + k] = s2;
+            cur_tok[r0 + k] = tok;
+        }
+    }
+}
+
 __global__ void count_done_kernel(const SelState* st, int B, int* out) {
     int c = 0;
     for (int i = threadIdx.x; i < B; i += blockDim.x) c += st[i].done;
@@ -470,17 +713,17 @@ __global__ void count_done_kernel(const SelState* st, int B, int* out) {
 __global__ void bump_kernel(int* p) { *p += 1; }
 }  // namespace
 
-int sel_state_bytes() { return (int)sizeof(SelState); }
 int sel_parts_bytes() { return (int)sizeof(SelPart) * SEL_SPLIT; }
+int beam_cand_bytes(int beam) { return (int)sizeof(BeamCand) * SEL_SPLIT * 2 * beam; }
 
 void launch_dec_self_attn(const float* part, int ks, const float* bias, h16* kc, h16* vc, const int* pos, int B,
-                          int H, int ctx, h16* out, hipStream_t s) {
-    dec_self_attn_kernel<<<dim3(H, B), 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out);
+                          int H, int ctx, h16* out, const int* anc, hipStream_t s) {
+    dec_self_attn_kernel<<<dim3(H, B), 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, anc);
 }
 
 void launch_dec_cross_attn(const float* part, int ks, const float* bias, const h16* xk, const h16* xv, int B, int H,
-                           int T, h16* out, hipStream_t s) {
-    dec_cross_attn_kernel<<<dim3(H, B), 256, 0, s>>>(part, ks, bias, xk, xv, H, B, T, out);
+                           int T, int beam, h16* out, hipStream_t s) {
+    dec_cross_attn_kernel<<<H * B, 256, 0, s>>>(part, ks, bias, xk, xv, H, B, T, beam, out);
 }
 
 void launch_dec_resid_ln(const float* part, int ks, int B, int D, const float* bias, float* x, const float* g,
@@ -495,21 +738,25 @@ void launch_dec_reduce_gelu(const float* part, int ks, int B, int N, const float
                                                                                                  bias, y);
 }
 
-void launch_select(const float* logits, int B, const int* pos, int prompt_len, int sot_pos, int lang_pos,
-                   int max_length, int V, int eot, int no_speech, int no_ts, int tb, int blank, int first_lang,
-                   int n_langs, int suppress_blank, int with_ts, int max_init_ts, const int* prompt,
-                   const unsigned* supmask, void* st, int* cur_tok, int* tokens, int max_tokens, void* sel_parts,
+void launch_select(const float* logits, int rows, const int* pos, const SelParams& P, const int* prompt,
+                   const unsigned* supmask, SelState* st, int* cur_tok, int* tokens, int max_tokens, void* sel_parts,
                    hipStream_t s) {
-    SelParams P{prompt_len, sot_pos, lang_pos, max_length, V, eot, no_speech, no_ts, tb, blank, first_lang,
-                n_langs, suppress_blank, with_ts, max_init_ts};
-    select_partial_kernel<<<dim3(B, SEL_SPLIT), 256, 0, s>>>(logits, P, pos, supmask, (const SelState*)st,
-                                                              (SelPart*)sel_parts);
-    select_final_kernel<<<B, 64, 0, s>>>(logits, P, pos, prompt, (const SelPart*)sel_parts, (SelState*)st, cur_tok,
-                                          tokens, max_tokens);
+    select_partial_kernel<<<dim3(rows, SEL_SPLIT), 256, 0, s>>>(logits, P, pos, supmask, st, (SelPart*)sel_parts);
+    select_final_kernel<<<rows, 64, 0, s>>>(logits, P, pos, prompt, (const SelPart*)sel_parts, st, cur_tok, tokens,
+                                             max_tokens);
 }
 
-void launch_count_done(const void* st, int B, int* out, hipStream_t s) {
-    count_done_kernel<<<1, 64, 0, s>>>((const SelState*)st, B, out);
+void launch_beam(const float* logits, int windows, const int* pos, const SelParams& P, const unsigned* supmask,
+                 SelState* st, const void* sel_parts, void* cand, int* seq, int* anc, int ctx, BeamWin* bw,
+                 int* best_tok, int* cur_tok, int max_tokens, hipStream_t s) {
+    beam_topk_kernel<<<dim3(windows * P.beam, SEL_SPLIT), 256, 0, s>>>(logits, P, pos, supmask, st,
+                                                                       (const SelPart*)sel_parts, (BeamCand*)cand);
+    beam_update_kernel<<<windows, 256, 0, s>>>(P, pos, st, (const BeamCand*)cand, seq, anc, ctx, bw, best_tok,
+                                                cur_tok, max_tokens);
+}
+
+void launch_count_done(const SelState* st, int rows, int* out, hipStream_t s) {
+    count_done_kernel<<<1, 64, 0, s>>>(st, rows, out);
 }
 
 void launch_bump(int* p, hipStream_t s) { bump_kernel<<<1, 1, 0, s>>>(p); }

@@ -19,6 +19,7 @@
 
 #include "../../include/osw.h"
 #include "common.h"
+#include "decode.h"
 
 namespace osw {
 // launchers from the other translation units
@@ -31,17 +32,14 @@ void launch_enc_attn(const h16*, h16*, int, int, int, hipStream_t);
 void launch_init_uniform(void*, bool, int64_t, uint64_t, float, float, int64_t, int64_t, hipStream_t);
 uint64_t hash_stream_key(uint64_t, int64_t);
 void launch_dec_embed(const h16*, const float*, const int*, const int*, int, int, int, float*, hipStream_t);
-void launch_dec_self_attn(const float*, int, const float*, h16*, h16*, const int*, int, int, int, h16*, hipStream_t);
-void launch_dec_cross_attn(const float*, int, const float*, const h16*, const h16*, int, int, int, h16*, hipStream_t);
+void launch_dec_self_attn(const float*, int, const float*, h16*, h16*, const int*, int, int, int, h16*, const int*,
+                          hipStream_t);
+void launch_dec_cross_attn(const float*, int, const float*, const h16*, const h16*, int, int, int, int, h16*,
+                           hipStream_t);
 void launch_dec_resid_ln(const float*, int, int, int, const float*, float*, const float*, const float*, h16*,
                          const h16*, const float*, const int*, const int*, int, hipStream_t);
 void launch_dec_reduce_gelu(const float*, int, int, int, const float*, h16*, hipStream_t);
-void launch_select(const float*, int, const int*, int, int, int, int, int, int, int, int, int, int, int, int, int, int,
-                   int, const int*, const unsigned*, void*, int*, int*, int, void*, hipStream_t);
-int sel_parts_bytes();
-void launch_count_done(const void*, int, int*, hipStream_t);
 void launch_bump(int*, hipStream_t);
-int sel_state_bytes();
 }  // namespace osw
 
 using namespace osw;
@@ -113,6 +111,7 @@ struct osw_ctx {
     hipStream_t stream = nullptr;
     osw_dims d{};
     int B = 0;    // max windows per call
+    int R = 0;    // decoder row capacity (windows x beam hypotheses)
     int C1 = 0;   // conv1 input channels padded to a multiple of 64
     std::vector<void*> owned;
     std::map<std::string, Tensor> w;
@@ -150,8 +149,12 @@ struct osw_ctx {
     float* logits = nullptr;
     int *cur_tok = nullptr, *pos = nullptr, *tokens = nullptr, *prompt = nullptr, *done = nullptr;
     unsigned* supmask = nullptr;
-    void* sel = nullptr;
-    void* selp = nullptr;      // per-window vocabulary-slice partial stats
+    SelState* sel = nullptr;   // per decoder row
+    void* selp = nullptr;      // per-row vocabulary-slice partial stats
+    int* anc = nullptr;        // beam: [R][ctx] row whose cache slot holds position p of this hypothesis
+    int* btok = nullptr;       // beam: [B][ctx] best finished hypothesis per window
+    BeamWin* bwin = nullptr;   // beam: [B]
+    void* bcand = nullptr;     // beam: [R][SEL_SPLIT][2*beam] candidates
     int* done_host = nullptr;  // pinned
     float* part = nullptr;     // split-K partial slabs of the decoder GEMMs
     int64_t part_floats = 0;
@@ -386,29 +389,35 @@ void setup_workspace(osw_ctx* c) {
     c->Hf = dalloc<h16>(Me * 4 * De, o);
     c->E = dalloc<h16>(Me * De, o);
     c->XKV = dalloc<h16>((int64_t)d.n_text_layer * 2 * Me * Dd, o);
-    c->xd = dalloc<float>(B * Dd, o);
-    c->xdn = dalloc<h16>(B * Dd, o);
-    c->dqkv = dalloc<h16>(B * 3 * Dd, o);
-    c->dattn = dalloc<h16>(B * Dd, o);
-    c->dq = dalloc<h16>(B * Dd, o);
-    c->dh = dalloc<h16>(B * 4 * Dd, o);
-    const int64_t kvn = (int64_t)d.n_text_layer * B * d.n_text_ctx * Dd;
+    const int64_t R = c->R;
+    c->xd = dalloc<float>(R * Dd, o);
+    c->xdn = dalloc<h16>(R * Dd, o);
+    c->dqkv = dalloc<h16>(R * 3 * Dd, o);
+    c->dattn = dalloc<h16>(R * Dd, o);
+    c->dq = dalloc<h16>(R * Dd, o);
+    c->dh = dalloc<h16>(R * 4 * Dd, o);
+    const int64_t kvn = (int64_t)d.n_text_layer * R * d.n_text_ctx * Dd;
     c->kc = dalloc<h16>(kvn, o);
     c->vc = dalloc<h16>(kvn, o);
-    c->logits = dalloc<float>(B * d.n_vocab, o);
-    c->cur_tok = dalloc<int>(B, o);
+    c->logits = dalloc<float>(R * d.n_vocab, o);
+    c->cur_tok = dalloc<int>(R, o);
     c->pos = dalloc<int>(1, o);
-    c->tokens = dalloc<int>(B * d.n_text_ctx, o);
-    c->prompt = dalloc<int>(B * d.n_text_ctx, o);
+    c->tokens = dalloc<int>(R * d.n_text_ctx, o);
+    c->prompt = dalloc<int>(R * d.n_text_ctx, o);
     c->done = dalloc<int>(1, o);
     c->supmask = dalloc<unsigned>((d.n_vocab + 31) / 32, o);
-    c->sel = dalloc<char>((size_t)B * sel_state_bytes(), o);
-    c->selp = dalloc<char>((size_t)B * sel_parts_bytes(), o);
+    c->sel = dalloc<SelState>(R, o);
+    c->selp = dalloc<char>((size_t)R * sel_parts_bytes(), o);
+    c->anc = dalloc<int>(R * d.n_text_ctx, o);
+    c->btok = dalloc<int>(B * d.n_text_ctx, o);
+    c->bwin = dalloc<BeamWin>(B, o);
+    c->bcand = dalloc<char>((size_t)R * beam_cand_bytes(MAX_BEAM), o);
     {
-        const int64_t Bm = std::min<int64_t>(B, 64);
+        const int64_t Bm = std::min<int64_t>(R, 64);
         const int64_t shapes[][2] = {{3 * Dd, Dd}, {Dd, Dd}, {4 * Dd, Dd}, {Dd, 4 * Dd}, {d.n_vocab, Dd}};
         for (auto& nk : shapes)
             c->part_floats = std::max<int64_t>(c->part_floats, skinny_ksplit((int)nk[0], (int)nk[1]) * Bm * nk[0]);
+        c->part_floats = std::max<int64_t>(c->part_floats, R * 4 * Dd);  // > 64 rows: one unsplit slab
         c->part = dalloc<float>(c->part_floats, o);
     }
     HIPCHK(hipHostMalloc((void**)&c->done_host, sizeof(int), 0));
@@ -520,13 +529,20 @@ void encode(osw_ctx* c, const osw_window* wins, int n) {
 // One decoder step for nb windows.  Every projection is a split-K skinny GEMM whose
 // partial slabs are reduced by the kernel that consumes them (self/cross attention
 // for q/k/v, residual+LayerNorm for the out-projections and fc2, GELU for fc1).
-void decoder_step(osw_ctx* c, int nb) {
+// nb = decoder rows (windows x beam); rows of one window are adjacent.
+void decoder_step(osw_ctx* c, int nb, int beam) {
     const osw_dims& d = c->d;
     const int D = d.n_text_state, H = d.n_text_head, L = d.n_text_layer, ctx = d.n_text_ctx;
-    const int64_t xkv_which = (int64_t)nb * H * T_ENC * 64;
+    const int64_t xkv_which = (int64_t)(nb / beam) * H * T_ENC * 64;
     const int64_t kv_layer = (int64_t)nb * H * ctx * 64;
-    REQUIRE(nb <= 64 && D <= 1280, "decoder step: nb <= 64 and D <= 1280");
+    REQUIRE(nb <= c->R && D <= 1280, "decoder step: rows <= capacity and D <= 1280");
+    // <= 64 rows: split-K skinny GEMM; more (beam search): one slab from the tiled GEMM
     auto partial = [&](const h16* A, int lda, const h16* Wt, int N, int K) {
+        if (nb > 64) {
+            REQUIRE((int64_t)nb * N <= c->part_floats, "decoder workspace too small");
+            launch_gemm(gemm_plain(A, lda, Wt, nullptr, nb, N, K, c->part, N, EPI_F32), c->stream);
+            return 1;
+        }
         GemmArgs g = gemm_plain(A, lda, Wt, nullptr, nb, N, K, nullptr, 0, EPI_F32);
         REQUIRE((int64_t)skinny_ksplit(N, K) * nb * N <= c->part_floats, "split-K workspace too small");
         return launch_gemm_skinny_partial(g, c->part, c->stream);
@@ -538,7 +554,7 @@ void decoder_step(osw_ctx* c, int nb) {
         const std::string p = "dec.l" + std::to_string(l);
         int ks = partial(c->xdn, D, WH(c, p + ".qkv.w"), 3 * D, D);
         launch_dec_self_attn(c->part, ks, WF(c, p + ".qkv.b"), c->kc + l * kv_layer, c->vc + l * kv_layer, c->pos, nb,
-                             H, ctx, c->dattn, c->stream);
+                             H, ctx, c->dattn, beam > 1 ? c->anc : nullptr, c->stream);
         ks = partial(c->dattn, D, WH(c, p + ".o.w"), D, D);
         launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".o.b"), c->xd, WF(c, p + ".ln2.g"), WF(c, p + ".ln2.b"),
                             c->xdn, nullptr, nullptr, nullptr, nullptr, ctx, c->stream);
@@ -546,7 +562,7 @@ void decoder_step(osw_ctx* c, int nb) {
         {
             Timed t(c, CL_XATTN, 2.0 * nb * H * (double)T_ENC * 64 * 2);
             launch_dec_cross_attn(c->part, ks, WF(c, p + ".xq.b"), c->XKV + (2 * l) * xkv_which,
-                                  c->XKV + (2 * l + 1) * xkv_which, nb, H, T_ENC, c->dattn, c->stream);
+                                  c->XKV + (2 * l + 1) * xkv_which, nb, H, T_ENC, beam, c->dattn, c->stream);
         }
         ks = partial(c->dattn, D, WH(c, p + ".xo.w"), D, D);
         launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".xo.b"), c->xd, WF(c, p + ".ln3.g"), WF(c, p + ".ln3.b"),
@@ -569,45 +585,79 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
     const int V = d.n_vocab;
     const int n_pre = o->n_prefix;
     REQUIRE(n_pre >= 0 && (n_pre == 0 || o->prefix_tokens), "bad prefix");
+    const int beam = std::max(1, o->beam_size);
+    REQUIRE(beam <= MAX_BEAM, "beam_size > 8");
+    const int rows = nb * beam;
+    REQUIRE(rows <= c->R, "windows x beam_size exceeds the decoder row capacity (5 x max_batch)");
+    REQUIRE(beam == 1 || !r->logits_dump, "logits dump is greedy-only");
+    REQUIRE(V <= SEL_SPLIT * 4096, "vocabulary too large for the selection kernels");
     const int P = n_pre + 3 + (o->without_timestamps ? 1 : 0);
     const int max_len = std::min(o->max_length > 0 ? o->max_length : d.n_text_ctx, d.n_text_ctx);
     REQUIRE(P < max_len, "prompt longer than max_length");
-    std::vector<int> prompt((size_t)nb * P);
-    for (int b = 0; b < nb; ++b) {
-        int* pr = &prompt[(size_t)b * P];
-        for (int i = 0; i < n_pre; ++i) pr[i] = o->prefix_tokens[(size_t)b * n_pre + i];
-        pr[n_pre] = o->sot;
-        pr[n_pre + 1] = o->language_tokens ? o->language_tokens[b] : o->language_token;  // -1: detect
-        pr[n_pre + 2] = o->task_token;
-        if (o->without_timestamps) pr[n_pre + 3] = o->no_timestamps;
-    }
+    // one prompt per decoder row (the beam rows of a window share it)
+    std::vector<int> prompt((size_t)rows * P);
+    for (int b = 0; b < nb; ++b)
+        for (int k = 0; k < beam; ++k) {
+            int* pr = &prompt[((size_t)b * beam + k) * P];
+            for (int i = 0; i < n_pre; ++i) pr[i] = o->prefix_tokens[(size_t)b * n_pre + i];
+            pr[n_pre] = o->sot;
+            pr[n_pre + 1] = o->language_tokens ? o->language_tokens[b] : o->language_token;  // -1: detect
+            pr[n_pre + 2] = o->task_token;
+            if (o->without_timestamps) pr[n_pre + 3] = o->no_timestamps;
+        }
     std::vector<unsigned> mask((V + 31) / 32, 0u);
     for (int i = 0; i < o->n_suppress; ++i) {
         const int t = o->suppress_tokens[i];
         if (t >= 0 && t < V) mask[t >> 5] |= 1u << (t & 31);
     }
-    std::vector<int> first(nb);
-    for (int b = 0; b < nb; ++b) first[b] = prompt[(size_t)b * P];
+    std::vector<int> first(rows);
+    for (int b = 0; b < rows; ++b) first[b] = prompt[(size_t)b * P];
     HIPCHK(hipMemcpyAsync(c->prompt, prompt.data(), prompt.size() * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->supmask, mask.data(), mask.size() * 4, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->cur_tok, first.data(), nb * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->cur_tok, first.data(), rows * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemsetAsync(c->pos, 0, 4, c->stream));
-    HIPCHK(hipMemsetAsync(c->sel, 0, (size_t)nb * sel_state_bytes(), c->stream));
+    HIPCHK(hipMemsetAsync(c->sel, 0, (size_t)rows * sizeof(SelState), c->stream));
     const int max_tok = std::max(1, max_len - P);
+    std::vector<int> anc0;
+    if (beam > 1) {
+        anc0.resize((size_t)rows * d.n_text_ctx);
+        for (int b = 0; b < rows; ++b)
+            for (int p = 0; p < d.n_text_ctx; ++p) anc0[(size_t)b * d.n_text_ctx + p] = b;
+        HIPCHK(hipMemcpyAsync(c->anc, anc0.data(), anc0.size() * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemsetAsync(c->bwin, 0, (size_t)nb * sizeof(BeamWin), c->stream));
+        HIPCHK(hipMemsetAsync(c->btok, 0, (size_t)nb * max_tok * 4, c->stream));
+    }
+    SelParams SP{};
+    SP.prompt_len = P; SP.sot_pos = n_pre; SP.lang_pos = n_pre + 1; SP.max_length = max_len;
+    SP.V = V; SP.eot = o->eot; SP.no_speech = o->no_speech; SP.no_ts = o->no_timestamps; SP.tb = o->timestamp_begin;
+    SP.blank = o->blank; SP.first_lang = o->first_lang; SP.n_langs = o->n_langs;
+    SP.suppress_blank = o->suppress_blank; SP.with_ts = o->without_timestamps ? 0 : 1;
+    SP.max_init_ts = o->max_initial_timestamp_index;
+    SP.beam = beam;
+    SP.num_hyp = std::max(1, o->num_hypotheses);
+    SP.max_cand = std::max(1, (int)std::lround(beam * (o->patience > 0.f ? o->patience : 1.f)));
+    SP.length_penalty = o->length_penalty;
+    auto select = [&] {
+        launch_select(c->logits, rows, c->pos, SP, c->prompt, c->supmask, c->sel, c->cur_tok, c->tokens, max_tok,
+                      c->selp, c->stream);
+        if (beam > 1)
+            launch_beam(c->logits, nb, c->pos, SP, c->supmask, c->sel, c->selp, c->bcand, c->tokens, c->anc,
+                        d.n_text_ctx, c->bwin, c->btok, c->cur_tok, max_tok, c->stream);
+    };
     auto one_step = [&] {
-        decoder_step(c, nb);
-        launch_select(c->logits, nb, c->pos, P, n_pre, n_pre + 1, max_len, V, o->eot, o->no_speech,
-                      o->no_timestamps, o->timestamp_begin, o->blank, o->first_lang, o->n_langs, o->suppress_blank,
-                      o->without_timestamps ? 0 : 1, o->max_initial_timestamp_index, c->prompt, c->supmask, c->sel,
-                      c->cur_tok, c->tokens, max_tok, c->selp, c->stream);
+        decoder_step(c, rows, beam);
+        select();
         launch_bump(c->pos, c->stream);
     };
     const int CH = 8;
     const bool graph = c->use_graph && !r->logits_dump;
     if (graph) {
+        int32_t lp_bits;
+        std::memcpy(&lp_bits, &SP.length_penalty, 4);
         std::vector<int64_t> key = {nb, P, n_pre, max_len, o->eot, o->no_speech, o->no_timestamps,
                                     o->timestamp_begin, o->blank, o->first_lang, o->n_langs, o->suppress_blank,
-                                    o->without_timestamps, o->max_initial_timestamp_index};
+                                    o->without_timestamps, o->max_initial_timestamp_index, beam, SP.num_hyp,
+                                    SP.max_cand, lp_bits};
         if (!c->dgraph || key != c->dgraph_key) {
             if (c->dgraph) {
                 HIPCHK(hipGraphExecDestroy(c->dgraph));
@@ -646,16 +696,12 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
             } else {
                 const int samp = steps - (P - 1);
                 if (r->logits_dump && samp >= 0 && samp < r->dump_steps) {
-                    decoder_step(c, nb);
+                    decoder_step(c, rows, beam);
                     for (int b = 0; b < nb; ++b)
                         HIPCHK(hipMemcpyAsync(r->logits_dump + ((size_t)b * r->dump_steps + samp) * V,
                                               c->logits + (size_t)b * V, (size_t)V * 4, hipMemcpyDeviceToHost,
                                               c->stream));
-                    launch_select(c->logits, nb, c->pos, P, n_pre, n_pre + 1, max_len, V, o->eot, o->no_speech,
-                                  o->no_timestamps, o->timestamp_begin, o->blank, o->first_lang, o->n_langs,
-                                  o->suppress_blank, o->without_timestamps ? 0 : 1, o->max_initial_timestamp_index,
-                                  c->prompt, c->supmask, c->sel, c->cur_tok, c->tokens, max_tok, c->selp,
-                                  c->stream);
+                    select();
                     launch_bump(c->pos, c->stream);
                 } else {
                     one_step();
@@ -667,30 +713,35 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
             since_check += did;
             if (steps >= P && (since_check >= CH || steps >= max_len)) {
                 since_check = 0;
-                launch_count_done(c->sel, nb, c->done, c->stream);
+                launch_count_done(c->sel, rows, c->done, c->stream);
                 HIPCHK(hipMemcpyAsync(c->done_host, c->done, 4, hipMemcpyDeviceToHost, c->stream));
                 HIPCHK(hipStreamSynchronize(c->stream));
-                if (*c->done_host >= nb) break;
+                if (*c->done_host >= rows) break;
             }
         }
     }
     c->pf.decode_steps = steps;
     // read back
-    std::vector<char> st((size_t)nb * sel_state_bytes());
+    std::vector<SelState> st(rows);
+    HIPCHK(hipMemcpyAsync(st.data(), c->sel, rows * sizeof(SelState), hipMemcpyDeviceToHost, c->stream));
     std::vector<int> toks((size_t)nb * max_tok);
-    HIPCHK(hipMemcpyAsync(st.data(), c->sel, st.size(), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(toks.data(), c->tokens, toks.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    std::vector<BeamWin> bw(nb);
+    if (beam > 1) {
+        HIPCHK(hipMemcpyAsync(toks.data(), c->btok, toks.size() * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(bw.data(), c->bwin, nb * sizeof(BeamWin), hipMemcpyDeviceToHost, c->stream));
+    } else {
+        HIPCHK(hipMemcpyAsync(toks.data(), c->tokens, toks.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    }
     HIPCHK(hipStreamSynchronize(c->stream));
-    struct S { int n_sampled, last, penult, last_ts, done, lang; float sum_lp, nsp; };
-    static_assert(sizeof(S) == 32, "SelState layout");
     for (int b = 0; b < nb; ++b) {
-        const S* sp = (const S*)&st[(size_t)b * sizeof(S)];
-        const int n = std::min(sp->n_sampled, std::min(max_tok, r->max_tokens));
+        const SelState& sp = st[(size_t)b * beam];
+        const int n0 = beam > 1 ? bw[b].best_len : sp.n_sampled;
+        const int n = std::min(n0, std::min(max_tok, r->max_tokens));
         r->n_tokens[b] = n;
         for (int i = 0; i < n; ++i) r->tokens[(size_t)b * r->max_tokens + i] = toks[(size_t)b * max_tok + i];
-        r->sum_logprob[b] = sp->sum_lp;
-        r->no_speech_prob[b] = sp->nsp;
-        r->language[b] = sp->lang;
+        r->sum_logprob[b] = beam > 1 ? bw[b].best_raw : sp.sum_lp;
+        r->no_speech_prob[b] = sp.nsp;
+        r->language[b] = sp.lang;
     }
 }
 
@@ -786,6 +837,7 @@ int osw_create(const osw_dims* dims, int32_t device, int32_t max_batch, osw_ctx*
         c->device = device;
         c->d = *dims;
         c->B = max_batch;
+        c->R = max_batch * 5;  // room for the reference's beam_size = 5 at full batch
         c->C1 = (dims->n_mels + 63) / 64 * 64;
         if (const char* e = std::getenv("OSW_NO_GRAPH")) c->use_graph = !(e[0] == '1');
         HIPCHK(hipSetDevice(device));

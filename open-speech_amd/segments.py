@@ -7,7 +7,8 @@ tokens — but the windows of DIFFERENT clips that are due at the same time are
 encoded and decoded together on the GPU (grouped by prompt length, since every
 window of one decode call shares its prompt length).
 
-Semantics restated (greedy, single temperature 0.0 — the reference passes a scalar
+Semantics restated (beam search width ``beam_size`` — 5 in the reference, 1 = greedy
+for the parity mode — and a single temperature 0.0: the reference passes a scalar
 ``temperature`` at ``src/backends/faster_whisper.py:238``, so there is no fallback):
   content_frames = n_frames - 1; segment_size = min(3000, content_frames - seek)
   prompt = [<|startofprev|>] + previous_tokens[-223:] (if any) + [sot, lang, task]
@@ -43,10 +44,14 @@ class TranscribeOptions:
     without_timestamps: bool = False
     max_initial_timestamp: float = 1.0
     temperature: float = 0.0
+    beam_size: int = 5             # faster-whisper / reference default (src/backends/faster_whisper.py:237)
+    patience: float = 1.0
+    length_penalty: float = 1.0
 
     def key(self):
         return (self.task, self.language, self.initial_prompt, self.condition_on_previous_text,
-                self.without_timestamps, tuple(self.suppress_tokens), self.suppress_blank)
+                self.without_timestamps, tuple(self.suppress_tokens), self.suppress_blank, self.beam_size,
+                self.patience, self.length_penalty)
 
 
 @dataclass
@@ -129,7 +134,8 @@ def transcribe_clips(engine, pcm_list: list, opts: TranscribeOptions, tok: Whisp
         s.done = s.content_frames <= 0
         states.append(s)
     max_init = int(round(opts.max_initial_timestamp / TIME_PRECISION))
-    B = engine.max_batch
+    beam = max(1, int(opts.beam_size))
+    B = max(1, min(engine.max_batch, getattr(engine, "max_rows", engine.max_batch) // beam))
     while True:
         active = [s for s in states if not s.done]
         if not active:
@@ -151,7 +157,8 @@ def transcribe_clips(engine, pcm_list: list, opts: TranscribeOptions, tok: Whisp
                 langs = None if _detect else [s.lang_token for s, _ in chunk]
                 cfg = DecodeConfig(task=opts.task, language_token=None, suppress_tokens=suppress,
                                    suppress_blank=opts.suppress_blank, without_timestamps=opts.without_timestamps,
-                                   max_initial_timestamp_index=max_init)
+                                   max_initial_timestamp_index=max_init, beam_size=beam, patience=opts.patience,
+                                   length_penalty=opts.length_penalty)
                 prefixes = [p for _, p in chunk] if _plen else None
                 outs = engine.decode(len(chunk), cfg, prefix=prefixes, languages=langs)
                 for (s, _), w, out in zip(chunk, wins, outs):

@@ -146,3 +146,107 @@ def greedy_from_encoder(oracle, xkv, st, *, language=None, task=None, prev_token
     del sot_index
     return WindowResult(tokens=sampled, sum_logprob=sum_lp, no_speech_prob=nsp, language=lang,
                         step_logits=step_logits, prompt_logits=prompt_logits)
+
+
+# ---------------------------------------------------------------------------
+# Beam search — restated from CTranslate2's ``BeamSearch::search`` (upstream
+# ``src/decoding.cc``, not vendored and not installed here; faster-whisper 1.2.1
+# calls it with ``beam_size=5, patience=1, length_penalty=1, num_hypotheses=1``
+# from ``generate_with_fallback`` for the reference's ``beam_size=5``,
+# ``src/backends/faster_whisper.py:237``).  PARITY UNPINNED: no CTranslate2 build or
+# beam-search fixture exists in this container, so this restatement (not CT2
+# output) is the checker for the HIP beam path.  Rules restated:
+#   * the first sampled step expands only the single prompt hypothesis;
+#   * candidates = top 2*beam of (cumulative score + processed log-prob) over
+#     beam x vocab, ordered by score desc, flat index (beam*V + token) asc;
+#   * of the first ``beam`` candidates, an <|endoftext|> one (or any one at the
+#     last step) is registered as a finished hypothesis with its cumulative score
+#     and its slot is refilled by the next non-EOT candidate from ranks >= beam;
+#   * stop when the last step is reached, or the rank-0 candidate finished this
+#     step and >= num_hypotheses are finished, or >= round(beam*patience) are;
+#   * result = the finished hypothesis with the highest score / len**length_penalty
+#     (len = its token count without EOT; first registered wins ties).
+# ---------------------------------------------------------------------------
+@dataclass
+class BeamOptions:
+    beam_size: int = 5
+    patience: float = 1.0
+    length_penalty: float = 1.0
+    num_hypotheses: int = 1
+
+
+def _norm_score(score: float, n: int, length_penalty: float) -> float:
+    if n == 0:
+        return -np.inf if length_penalty != 0 else score
+    return score / (float(n) ** length_penalty)
+
+
+def beam_from_encoder(oracle, xkv, st, *, language=None, task=None, prev_tokens=(),
+                      opts: DecodeOptions = DecodeOptions(), beam: BeamOptions = BeamOptions()) -> WindowResult:
+    import copy
+
+    task = st.transcribe if task is None else task
+    cache = oracle.new_cache()
+    prompt = []
+    if prev_tokens:
+        prompt.append(st.sot_prev)
+        prompt.extend(list(prev_tokens)[-(opts.max_length // 2 - 1):])
+    prompt.append(st.sot)
+    pos = 0
+    for t in prompt:
+        lg = oracle.decoder_step(t, pos, cache, xkv)
+        pos += 1
+    raw_sot = lg
+    lang = detect_language(raw_sot, st) if language is None else language
+    nsp = no_speech_prob(raw_sot, st)
+    rest = [lang, task] + ([st.no_timestamps] if opts.without_timestamps else [])
+    for t in rest:
+        lg = oracle.decoder_step(t, pos, cache, xkv)
+        pos += 1
+    prompt_len = len(prompt) + len(rest)
+    K = beam.beam_size
+    V = lg.shape[0]
+    max_cand = int(round(K * beam.patience))
+    alive = [([], 0.0, cache, lg)]        # (tokens, cumulative score, kv cache, next-token logits)
+    finished = []                         # (normalised, raw score, tokens)
+    n = 0
+    while True:
+        is_last = prompt_len + n + 1 >= opts.max_length
+        scores = []
+        for k, (seq, cum, _, logit) in enumerate(alive):
+            x = process_logits(logit, seq, st, opts)
+            lp = log_softmax(x).astype(np.float32)
+            scores.append(np.float32(cum) + lp)
+        flat = np.concatenate(scores)
+        order = np.lexsort((np.arange(flat.size), -flat.astype(np.float64)))[:2 * K]
+        cands = [(float(flat[i]), int(i) // V, int(i) % V) for i in order]
+        chosen, sec, top_fin = [], K, False
+        for k in range(K):
+            s, q, tok = cands[k]
+            nb = k
+            if tok == st.eot or is_last:
+                if k == 0:
+                    top_fin = True
+                toks = list(alive[q][0]) + ([] if tok == st.eot else [tok])
+                finished.append((_norm_score(s, len(toks), beam.length_penalty), s, toks))
+                for j in range(sec, 2 * K):
+                    if cands[j][2] != st.eot:
+                        nb, sec = j, j + 1
+                        break
+            chosen.append(cands[nb])
+        if is_last or (top_fin and len(finished) >= beam.num_hypotheses) or len(finished) >= max_cand:
+            break
+        nxt = []
+        for s, q, tok in chosen:
+            seq, _, cch, _ = alive[q]
+            c2 = copy.deepcopy(cch)
+            logit = oracle.decoder_step(tok, pos, c2, xkv)
+            nxt.append((list(seq) + [tok], s, c2, logit))
+        alive = nxt
+        pos += 1
+        n += 1
+    best = finished[0]
+    for f in finished[1:]:
+        if f[0] > best[0]:
+            best = f
+    return WindowResult(tokens=best[2], sum_logprob=best[1], no_speech_prob=nsp, language=lang)

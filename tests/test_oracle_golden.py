@@ -113,3 +113,39 @@ def test_synth_clip_levels():
     assert pcm.dtype == np.int16 and len(pcm) == 480000
     rms = np.sqrt(np.mean((pcm / 32768.0) ** 2))
     assert abs(20 * np.log10(rms) + 18.0) < 0.5
+
+
+def test_beam_width1_equals_greedy(tiny):
+    """The beam restatement at width 1 reduces to greedy decoding (same ids, same
+    cumulative log-prob) — a self-consistency pin for the unpinned beam oracle."""
+    d, w, z = tiny
+    st = D.SpecialTokens.for_vocab(d.n_vocab)
+    orc = WhisperOracle(d, w, fp16=False)
+    sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+    opts = odec.DecodeOptions(suppress_tokens=sup, max_length=24)
+    xkv = orc.cross_kv(orc.encode(z["mel"]))
+    g = odec.greedy_from_encoder(orc, xkv, st, opts=opts)
+    b = odec.beam_from_encoder(orc, xkv, st, opts=opts, beam=odec.BeamOptions(beam_size=1))
+    assert b.tokens == g.tokens
+    assert abs(b.sum_logprob - g.sum_logprob) < 1e-4 * max(1.0, abs(g.sum_logprob))
+
+
+def test_beam_width5_obeys_rules(tiny):
+    """Width 5: the hypothesis it returns obeys the logits rules it was decoded under."""
+    d, w, z = tiny
+    st = D.SpecialTokens.for_vocab(d.n_vocab)
+    orc = WhisperOracle(d, w, fp16=False)
+    sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+    opts = odec.DecodeOptions(suppress_tokens=sup, max_length=24)
+    xkv = orc.cross_kv(orc.encode(z["mel"]))
+    b = odec.beam_from_encoder(orc, xkv, st, opts=opts, beam=odec.BeamOptions(beam_size=5))
+    assert b.tokens and b.tokens[0] >= st.timestamp_begin
+    ts = [t for t in b.tokens if t >= st.timestamp_begin]
+    assert ts == sorted(ts)
+    # replay the structural rules (timestamp logits far below text ones, so the
+    # logit-dependent mass rule stays off): every chosen token must be allowed
+    probe = np.zeros(d.n_vocab, np.float32)
+    probe[st.timestamp_begin:] = -100.0
+    for i, t in enumerate(b.tokens):
+        x = odec.process_logits(probe, b.tokens[:i], st, opts)
+        assert np.isfinite(x[t]), (i, t)

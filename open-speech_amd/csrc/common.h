@@ -60,6 +60,7 @@ struct GemmArgs {
     int epi;
     int heads_T, heads_H, heads_nb;      // EPI_HEADS geometry
     int band;                            // 256-tile walk: column band width (0 = all columns)
+    int kc;                              // 128-tile split-K: K per blockIdx.z, EPI_F32 slab z at C + z*M*ldc (0 = K)
 };
 
 // launchers (defined in the .hip files)
@@ -68,6 +69,8 @@ void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s);  // 0 a
 // M <= 64, K % 128 == 0; `part` needs skinny_ksplit(N,K)*M*N floats
 void launch_gemm_skinny(const GemmArgs& g, float* part, hipStream_t s);
 int skinny_ksplit(int N, int K);
+int tiled_ksplit(int M, int N, int K);
+void launch_gemm_tiled_partial(const GemmArgs& g, float* part, int ks, hipStream_t s);
 int launch_gemm_skinny_partial(const GemmArgs& g, float* part, hipStream_t s);
 void launch_layernorm(const float* x, int64_t M, int D, const float* g, const float* b, h16* y, hipStream_t s);
 

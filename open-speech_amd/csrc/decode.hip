@@ -516,23 +516,31 @@ __device__ __forceinline__ ArgMax block_amax(ArgMax a, ArgMax* red) {
     return r;
 }
 
-constexpr int BEAM_SLICE = 4096;  // >= ceil(V / SEL_SPLIT) for V <= 65536
+constexpr int BEAM_SLICES = 4;   // vocabulary slices per row in beam_topk
+constexpr int MAXK2 = 2 * MAX_BEAM;
 
-// grid (rows, SEL_SPLIT), 256 threads: top 2*beam (score, flat) of one vocabulary slice
+__device__ __forceinline__ bool cand_better(float s, int i, float t, int j) {
+    return s > t || (s == t && i < j);
+}
+
+// grid (rows, BEAM_SLICES), 256 threads: the top 2*beam (score desc, flat index asc)
+// of one vocabulary slice of one row.  Each thread keeps a sorted list of its own
+// best 2*beam entries in registers (insertion, visited in index order), then the
+// lists are merged pairwise through LDS in 8 levels.
 __global__ __launch_bounds__(256) void beam_topk_kernel(const float* __restrict__ logits, SelParams P,
                                                         const int* __restrict__ pos_ptr,
                                                         const unsigned* __restrict__ supmask,
                                                         const SelState* __restrict__ st,
                                                         const SelPart* __restrict__ parts, BeamCand* __restrict__ cand) {
-    __shared__ float sc[BEAM_SLICE];
     __shared__ float stat[3];
-    __shared__ ArgMax red[4];
+    __shared__ float lv[256][MAXK2 + 1];
+    __shared__ int li[256][MAXK2 + 1];
     const int row = blockIdx.x, sl = blockIdx.y, tid = threadIdx.x;
     const int step = *pos_ptr;
     const SelState s = st[row];
     if (sel_mode(P, step, s) != SEL_SAMPLE) return;
     const int K2 = 2 * P.beam, k = row % P.beam;
-    BeamCand* out = cand + ((int64_t)row * SEL_SPLIT + sl) * K2;
+    BeamCand* out = cand + ((int64_t)row * BEAM_SLICES + sl) * K2;
     if (step == P.prompt_len - 1 && k != 0) {  // first sampled step: only the prompt hypothesis expands
         if (tid < K2) out[tid] = BeamCand{-INFINITY, INT_MAX};
         return;
@@ -549,29 +557,63 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(const float* __restrict_
     const float lse_all = stat[0], lse_ts = stat[1];
     const bool ts_wins = stat[2] != 0.f;
     const RowRules R = row_rules(P, s);
-    const int per = (P.V + SEL_SPLIT - 1) / SEL_SPLIT;
+    const int per = (P.V + BEAM_SLICES - 1) / BEAM_SLICES;
     const int lo = sl * per, hi = min(P.V, lo + per);
     const float* x = logits + (int64_t)row * P.V;
+    float tv[MAXK2];
+    int ti[MAXK2];
+#pragma unroll
+    for (int j = 0; j < MAXK2; ++j) { tv[j] = -INFINITY; ti[j] = INT_MAX; }
+    const int base = k * P.V;
     for (int v = lo + tid; v < hi; v += 256) {
         float lp = -INFINITY;
         if (!tok_masked(P, R, supmask, v)) {
             if (!ts_wins) lp = x[v] - lse_all;
             else if (v >= P.tb) lp = x[v] - lse_ts;
         }
-        sc[v - lo] = s.sum_lp + lp;
+        const float sc = s.sum_lp + lp;
+        const int id = base + v;
+        if (!cand_better(sc, id, tv[MAXK2 - 1], ti[MAXK2 - 1])) continue;
+        bool placed = false;
+#pragma unroll
+        for (int j = MAXK2 - 1; j >= 0; --j) {
+            if (!placed) {
+                if (j > 0 && cand_better(sc, id, tv[j - 1], ti[j - 1])) {
+                    tv[j] = tv[j - 1];
+                    ti[j] = ti[j - 1];
+                } else {
+                    tv[j] = sc;
+                    ti[j] = id;
+                    placed = true;
+                }
+            }
+        }
     }
+#pragma unroll
+    for (int j = 0; j < MAXK2; ++j) { lv[tid][j] = tv[j]; li[tid][j] = ti[j]; }
     __syncthreads();
-    const int base = k * P.V + lo;
-    for (int r = 0; r < K2; ++r) {
-        ArgMax a{-INFINITY, INT_MAX};
-        for (int i = tid; i < hi - lo; i += 256) a = amax(a, ArgMax{sc[i], base + i});  // NaN = taken
-        a = block_amax(a, red);
-        if (tid == 0) {
-            out[r] = BeamCand{a.v, a.i};
-            if (a.i != INT_MAX) sc[a.i - base] = __builtin_nanf("");
+    for (int half = 128; half >= 1; half >>= 1) {  // merge list tid + half into list tid
+        if (tid < half) {
+            float mv[MAXK2];
+            int mi[MAXK2];
+            int a = 0, b = 0;
+#pragma unroll
+            for (int j = 0; j < MAXK2; ++j) {
+                if (j < K2) {
+                    const bool ta = cand_better(lv[tid][a], li[tid][a], lv[tid + half][b], li[tid + half][b]);
+                    mv[j] = ta ? lv[tid][a] : lv[tid + half][b];
+                    mi[j] = ta ? li[tid][a] : li[tid + half][b];
+                    a += ta;
+                    b += !ta;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < MAXK2; ++j)
+                if (j < K2) { lv[tid][j] = mv[j]; li[tid][j] = mi[j]; }
         }
         __syncthreads();
     }
+    if (tid < K2) out[tid] = BeamCand{lv[0][tid], li[0][tid]};
 }
 
 // grid windows, 256 threads: merge the candidates, register finished hypotheses,
@@ -582,7 +624,7 @@ __global__ __launch_bounds__(256) void beam_update_kernel(SelParams P, const int
                                                           int* __restrict__ anc, int ctx, BeamWin* __restrict__ bwin,
                                                           int* __restrict__ best_tok, int* __restrict__ cur_tok,
                                                           int max_tokens) {
-    constexpr int MAXC = MAX_BEAM * SEL_SPLIT * 2 * MAX_BEAM;
+    constexpr int MAXC = MAX_BEAM * BEAM_SLICES * MAXK2;
     __shared__ float cs[MAXC];
     __shared__ int ci[MAXC];
     __shared__ BeamCand top[2 * MAX_BEAM];
@@ -595,9 +637,9 @@ __global__ __launch_bounds__(256) void beam_update_kernel(SelParams P, const int
     const int r0 = w * K;
     const int step = *pos_ptr;
     if (sel_mode(P, step, st[r0]) != SEL_SAMPLE) return;
-    const int nc = K * SEL_SPLIT * K2;
+    const int nc = K * BEAM_SLICES * K2;
     for (int i = tid; i < nc; i += 256) {
-        const BeamCand c = cand[(int64_t)r0 * SEL_SPLIT * K2 + i];
+        const BeamCand c = cand[(int64_t)r0 * BEAM_SLICES * K2 + i];
         cs[i] = c.s;
         ci[i] = c.i;
     }
@@ -714,7 +756,7 @@ __global__ void bump_kernel(int* p) { *p += 1; }
 }  // namespace
 
 int sel_parts_bytes() { return (int)sizeof(SelPart) * SEL_SPLIT; }
-int beam_cand_bytes(int beam) { return (int)sizeof(BeamCand) * SEL_SPLIT * 2 * beam; }
+int beam_cand_bytes(int beam) { return (int)sizeof(BeamCand) * BEAM_SLICES * 2 * beam; }
 
 void launch_dec_self_attn(const float* part, int ks, const float* bias, h16* kc, h16* vc, const int* pos, int B,
                           int H, int ctx, h16* out, const int* anc, hipStream_t s) {
@@ -749,7 +791,7 @@ void launch_select(const float* logits, int rows, const int* pos, const SelParam
 void launch_beam(const float* logits, int windows, const int* pos, const SelParams& P, const unsigned* supmask,
                  SelState* st, const void* sel_parts, void* cand, int* seq, int* anc, int ctx, BeamWin* bw,
                  int* best_tok, int* cur_tok, int max_tokens, hipStream_t s) {
-    beam_topk_kernel<<<dim3(windows * P.beam, SEL_SPLIT), 256, 0, s>>>(logits, P, pos, supmask, st,
+    beam_topk_kernel<<<dim3(windows * P.beam, BEAM_SLICES), 256, 0, s>>>(logits, P, pos, supmask, st,
                                                                        (const SelPart*)sel_parts, (BeamCand*)cand);
     beam_update_kernel<<<windows, 256, 0, s>>>(P, pos, st, (const BeamCand*)cand, seq, anc, ctx, bw, best_tok,
                                                 cur_tok, max_tokens);

@@ -61,6 +61,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
     __shared__ __attribute__((aligned(16))) h16 lds[2][2][BM * BK];  // [buf][A|W], 64 KiB
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+    const int kc = g.kc > 0 ? g.kc : g.K, kbeg = blockIdx.z * kc;  // split-K: slab blockIdx.z
 
     // per-thread source rows for the 4 A and 4 W glds pieces (fixed over K)
     const h16* asrc[4];
@@ -71,8 +72,8 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
         const int c = swz(r, lane & 7);
         const int gm = min(m0 + r, g.M - 1);
         const int gn = min(n0 + r, g.N - 1);
-        asrc[i] = grp_row(g.A, gm, g.a_grp_rows, g.a_grp_stride, g.lda) + c * 8;
-        wsrc[i] = g.W + (int64_t)gn * g.ldw + c * 8;
+        asrc[i] = grp_row(g.A, gm, g.a_grp_rows, g.a_grp_stride, g.lda) + c * 8 + kbeg;
+        wsrc[i] = g.W + (int64_t)gn * g.ldw + c * 8 + kbeg;
     }
 
     auto stage = [&](int buf, int k0) {
@@ -92,7 +93,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    const int nk = g.K / BK;
+    const int nk = kc / BK;
     stage(0, 0);
     __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) & lgkmcnt(0)
     __syncthreads();
@@ -125,6 +126,22 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
         __syncthreads();
     }
 
+    if (EPI == EPI_F32 && g.kc > 0) {  // split-K partial slab: plain stores, no bias
+        float* C = (float*)g.C + (int64_t)blockIdx.z * g.M * g.ldc;
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int m = m0 + wm * 64 + mi * 16 + (lane >> 4) * 4 + i;
+                if (m >= g.M) continue;
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni) {
+                    const int n = n0 + wn * 64 + ni * 16 + (lane & 15);
+                    if (n < g.N) C[(int64_t)m * g.ldc + n] = acc[mi][ni][i];
+                }
+            }
+        return;
+    }
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
@@ -708,6 +725,33 @@ int launch_gemm_skinny_partial(const GemmArgs& g, float* part, hipStream_t s) {
         default: gemm_skinny_kernel<4, false, EPI_F32><<<grid, 256, 0, s>>>(g, kc, part); break;
     }
     return ks;
+}
+
+// Mid-size M (beam-search decoder rows, 65..~640): 128x128 tiles split over K so
+// the grid still fills the chip; each split writes its own fp32 slab, reduced by
+// the consumer kernel exactly like the skinny kernel's slabs.  Picks the largest
+// split (K/ks a multiple of 256... or 64) that keeps the grid near 512 workgroups.
+int tiled_ksplit(int M, int N, int K) {
+    const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    int best = 1;
+    for (int ks = 1; ks <= K / BK; ++ks) {
+        if (K % ks || (K / ks) % BK) continue;
+        if ((K / ks) < 256 && ks > 1) break;
+        if (tiles * ks > 640) break;
+        best = ks;
+    }
+    return best;
+}
+
+void launch_gemm_tiled_partial(const GemmArgs& g0, float* part, int ks, hipStream_t s) {
+    GemmArgs g = g0;
+    g.kc = g.K / ks;
+    g.C = part;
+    g.ldc = g.N;
+    g.bias = nullptr;
+    g.epi = EPI_F32;
+    dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, ks);
+    gemm_kernel<EPI_F32><<<grid, NTHR, 0, s>>>(g);
 }
 
 void launch_gemm_skinny(const GemmArgs& g, float* part, hipStream_t s) {

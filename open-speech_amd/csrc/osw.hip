@@ -417,7 +417,10 @@ void setup_workspace(osw_ctx* c) {
         const int64_t shapes[][2] = {{3 * Dd, Dd}, {Dd, Dd}, {4 * Dd, Dd}, {Dd, 4 * Dd}, {d.n_vocab, Dd}};
         for (auto& nk : shapes)
             c->part_floats = std::max<int64_t>(c->part_floats, skinny_ksplit((int)nk[0], (int)nk[1]) * Bm * nk[0]);
-        c->part_floats = std::max<int64_t>(c->part_floats, R * 4 * Dd);  // > 64 rows: one unsplit slab
+        for (auto& nk : shapes)  // > 64 rows: split-K slabs of the tiled GEMM
+            if (R > 64 && nk[0] != d.n_vocab)
+                c->part_floats = std::max<int64_t>(c->part_floats,
+                                                   (int64_t)tiled_ksplit((int)R, (int)nk[0], (int)nk[1]) * R * nk[0]);
         c->part = dalloc<float>(c->part_floats, o);
     }
     HIPCHK(hipHostMalloc((void**)&c->done_host, sizeof(int), 0));
@@ -539,9 +542,11 @@ void decoder_step(osw_ctx* c, int nb, int beam) {
     // <= 64 rows: split-K skinny GEMM; more (beam search): one slab from the tiled GEMM
     auto partial = [&](const h16* A, int lda, const h16* Wt, int N, int K) {
         if (nb > 64) {
-            REQUIRE((int64_t)nb * N <= c->part_floats, "decoder workspace too small");
-            launch_gemm(gemm_plain(A, lda, Wt, nullptr, nb, N, K, c->part, N, EPI_F32), c->stream);
-            return 1;
+            const int ks = tiled_ksplit(nb, N, K);
+            REQUIRE((int64_t)ks * nb * N <= c->part_floats, "decoder workspace too small");
+            launch_gemm_tiled_partial(gemm_plain(A, lda, Wt, nullptr, nb, N, K, nullptr, 0, EPI_F32), c->part, ks,
+                                      c->stream);
+            return ks;
         }
         GemmArgs g = gemm_plain(A, lda, Wt, nullptr, nb, N, K, nullptr, 0, EPI_F32);
         REQUIRE((int64_t)skinny_ksplit(N, K) * nb * N <= c->part_floats, "split-K workspace too small");

@@ -110,6 +110,15 @@ int osw_device_count(int32_t* out);
 
 int osw_create(const osw_dims* dims, int32_t device, int32_t max_batch, osw_ctx** out);
 int osw_destroy(osw_ctx* ctx);
+/* A second context on the parent's device that SHARES the parent's (finalized)
+ * weights but owns its stream, workspaces and decode state.  Two contexts per GPU
+ * driven from two host threads overlap one batch's MFMA-bound encoder with the
+ * other's HBM/latency-bound decoder (the faster-whisper reference runs one
+ * WhisperModel per process, src/backends/faster_whisper.py:40-45; this is the
+ * batcher's per-GPU lane, not a reference entry point).  The weights stay alive
+ * until the last context sharing them is destroyed; weight setters on a sibling
+ * return OSW_EINVAL. */
+int osw_create_sibling(osw_ctx* parent, int32_t max_batch, osw_ctx** out);
 
 /* Upload one canonical tensor (names and dtypes: open-speech_amd/weights.py). */
 int osw_set_weight(osw_ctx* ctx, const char* name, const void* host, int64_t nbytes);

@@ -31,6 +31,8 @@ struct BeamWin {
 };
 
 constexpr int MAX_BEAM = 8;
+constexpr int XPART = 72;     // floats per (decoder row, head, key chunk) cross-attention partial: m, l, pad, acc[64]
+constexpr int XCHUNKS = 8;    // fixed key chunks per (window, head) in cross-attention
 constexpr int SEL_SPLIT = 16;  // vocabulary slices per row in the selection kernels
 
 void launch_select(const float* logits, int rows, const int* pos, const SelParams& P, const int* prompt,

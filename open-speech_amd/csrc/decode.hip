@@ -9,6 +9,7 @@
 #include "decode.h"
 
 #include <climits>
+#include <cstdlib>
 
 namespace osw {
 
@@ -202,6 +203,177 @@ __global__ __launch_bounds__(256) void dec_cross_attn_kernel(const float* __rest
     reduce_head(part, ks, (int64_t)B * D, (int64_t)b * D + h * HD, bias, h * HD, q16, red4);
     const int64_t hoff = ((int64_t)w * H + h) * T * HD;
     attend_one<1536>(q16, xk + hoff, xv + hoff, T, out + (int64_t)b * D + h * HD);
+}
+
+// ---------------------------------------------------------------------------
+// Cross-attention split over fixed key chunks (flash-decoding).  The T = 1500 keys
+// of a (window, head) are cut into XCH = 8 fixed chunks of <= 192 keys; one
+// workgroup per (window, head, chunk) serves all `beam` decoder rows of the window.
+// Every lane first issues its 6 K and 6 V row pieces (12 x 16 B; 48 KB per
+// workgroup, the whole chunk in one HBM round trip), then reduces the rows' q from
+// the q projection's split-K slabs while the loads land.  Per row it writes the
+// chunk max m, l = Σ exp(s - m) and the unnormalised Σ exp(s - m)·v to a workspace
+// and takes an arrival ticket; the last workgroup of the (window, head) merges the
+// 8 chunks in fixed chunk order, so the output does not depend on the batch size or
+// the dispatch order.  Small batches get 8x the workgroups of one-per-(row, head)
+// (B = 1: 160 instead of 20), and beam rows read each K/V chunk once, not per row.
+// Chunks of one (window, head) go to the same XCD (bid % 8), so the partials and
+// the ticket stay in one L2.
+// Lane map: kg = tid >> 3 (32 key groups), c = tid & 7 (dims 8c..8c+7); the lane
+// holds keys u*32 + kg (u = 0..5) of the chunk for both scores and P·V.
+constexpr int XCH = XCHUNKS, XKEYS = 192, XU = XKEYS / 32;
+static_assert(XCH == 8, "the (window, head) -> XCD map assumes 8 chunks");
+
+template <int NB>
+__global__ __launch_bounds__(256) void dec_xattn_chunk_kernel(const float* __restrict__ part, int ks,
+                                                              const float* __restrict__ bias,
+                                                              const h16* __restrict__ xk, const h16* __restrict__ xv,
+                                                              int H, int W, int T, int beam, float* __restrict__ ws,
+                                                              int* __restrict__ ticket, h16* __restrict__ out) {
+    __shared__ float red[4][NB][HD];
+    __shared__ float rm[4][NB], rl[4][NB];
+    __shared__ float qsh[NB][HD];
+    __shared__ int is_last;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, kg = tid >> 3, c = tid & 7;
+    const int bid = blockIdx.x;
+    const int chunk = (bid >> 3) & 7;
+    const int p = (bid & 7) + 8 * (bid >> 6);  // (window, head) pair; its 8 chunks share bid % 8
+    if (p >= W * H) return;
+    const int h = p % H, w = p / H;
+    const int D = H * HD;
+    const int per = (T + XCH - 1) / XCH;
+    const int k0 = chunk * per, nk = min(T, k0 + per) - k0;
+    const int64_t hoff = ((int64_t)w * H + h) * T * HD;
+    h16x8 kf[XU], vf[XU];
+#pragma unroll
+    for (int u = 0; u < XU; ++u) {
+        const int key = k0 + min(u * 32 + kg, nk - 1);
+        kf[u] = *(const h16x8*)(xk + hoff + (int64_t)key * HD + 8 * c);
+        vf[u] = *(const h16x8*)(xv + hoff + (int64_t)key * HD + 8 * c);
+    }
+    // q of row r0 + k: fp16(bias + Σ split-K partials) / sqrt(64), the order of reduce_head
+    const int r0 = w * beam;
+    const int64_t slab = (int64_t)W * beam * D;
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+        if (k >= beam) break;
+        const int64_t off = (int64_t)(r0 + k) * D + h * HD + lane;
+        float v = 0.f;
+        int s = wv;
+        for (; s + 4 < ks; s += 8) v += part[s * slab + off] + part[(s + 4) * slab + off];
+        if (s < ks) v += part[s * slab + off];
+        red[wv][k][lane] = v;
+    }
+    __syncthreads();
+    if (wv == 0) {
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            if (k >= beam) break;
+            float r = bias[h * HD + lane];
+            r += red[0][k][lane] + red[1][k][lane] + red[2][k][lane] + red[3][k][lane];
+            qsh[k][lane] = (float)(h16)r * 0.125f;
+        }
+    }
+    __syncthreads();
+    // scores (8 lanes per key, combined by 3 xor-shuffles) and the chunk max per row
+    float sc[NB][XU], mx[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+        mx[k] = -INFINITY;
+        if (k >= beam) continue;
+        float q[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) q[i] = qsh[k][8 * c + i];
+#pragma unroll
+        for (int u = 0; u < XU; ++u) {
+            float d = 0.f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) d = fmaf((float)kf[u][i], q[i], d);
+            d += __shfl_xor(d, 1, 64);
+            d += __shfl_xor(d, 2, 64);
+            d += __shfl_xor(d, 4, 64);
+            sc[k][u] = d;
+            if (u * 32 + kg < nk) mx[k] = fmaxf(mx[k], d);
+        }
+        mx[k] = wave_max(mx[k]);
+        if (lane == 0) rm[wv][k] = mx[k];
+    }
+    __syncthreads();
+    // p = exp(s - m) (0 past the chunk end); l = Σ p (one lane per key); P·V per lane
+    float acc[NB][8], ls[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+        ls[k] = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[k][e] = 0.f;
+        if (k >= beam) continue;
+        const float m = fmaxf(fmaxf(rm[0][k], rm[1][k]), fmaxf(rm[2][k], rm[3][k]));
+        mx[k] = m;
+#pragma unroll
+        for (int u = 0; u < XU; ++u) {
+            const float pu = u * 32 + kg < nk ? __expf(sc[k][u] - m) : 0.f;
+            ls[k] += pu;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[k][e] = fmaf(pu, (float)vf[u][e], acc[k][e]);
+        }
+        // the 8 key groups of this wave: lanes c + 8 kr, kr = 0..7
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            float a = acc[k][e];
+            a += __shfl_xor(a, 8, 64);
+            a += __shfl_xor(a, 16, 64);
+            a += __shfl_xor(a, 32, 64);
+            acc[k][e] = a;
+        }
+        float l = c == 0 ? ls[k] : 0.f;
+        l = wave_sum(l);
+        if (lane == 0) rl[wv][k] = l;
+        if (lane < 8) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) red[wv][k][8 * c + e] = acc[k][e];
+        }
+    }
+    __syncthreads();
+    if (wv == 0) {
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            if (k >= beam) break;
+            float* dst = ws + (((int64_t)(r0 + k) * H + h) * XCH + chunk) * XPART;
+            dst[4 + lane] = (red[0][k][lane] + red[1][k][lane]) + (red[2][k][lane] + red[3][k][lane]);
+            if (lane == 0) {
+                dst[0] = mx[k];
+                dst[1] = (rl[0][k] + rl[1][k]) + (rl[2][k] + rl[3][k]);
+            }
+        }
+    }
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) {
+        const int old = atomicAdd(&ticket[p], 1);
+        is_last = old == XCH - 1;
+        if (old == XCH - 1) ticket[p] = 0;  // every chunk has arrived: reset for the next launch
+    }
+    __syncthreads();
+    if (!is_last) return;
+    __threadfence();
+    for (int k = wv; k < beam; k += 4) {
+        const float* src = ws + ((int64_t)(r0 + k) * H + h) * XCH * XPART;
+        float mm[XCH];
+        float M = -INFINITY;
+#pragma unroll
+        for (int s = 0; s < XCH; ++s) {
+            mm[s] = __hip_atomic_load(src + s * XPART, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            M = fmaxf(M, mm[s]);
+        }
+        float L = 0.f, O = 0.f;
+#pragma unroll
+        for (int s = 0; s < XCH; ++s) {
+            const float e = __expf(mm[s] - M);
+            L = fmaf(__hip_atomic_load(src + s * XPART + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), e, L);
+            O = fmaf(__hip_atomic_load(src + s * XPART + 4 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), e, O);
+        }
+        out[(int64_t)(r0 + k) * D + h * HD + lane] = (h16)(O / L);
+    }
 }
 
 // grid B, 1024 threads: x[b] += bias + Σ split-K partials (residual stream, fp32),
@@ -764,8 +936,22 @@ void launch_dec_self_attn(const float* part, int ks, const float* bias, h16* kc,
 }
 
 void launch_dec_cross_attn(const float* part, int ks, const float* bias, const h16* xk, const h16* xv, int B, int H,
-                           int T, int beam, h16* out, hipStream_t s) {
-    dec_cross_attn_kernel<<<H * B, 256, 0, s>>>(part, ks, bias, xk, xv, H, B, T, beam, out);
+                           int T, int beam, h16* out, float* ws, int* ticket, hipStream_t s) {
+    static const bool legacy = std::getenv("OSW_XATTN_LEGACY") != nullptr;  // A/B switch: one workgroup per (row, head)
+    if (legacy || !ws) {
+        dec_cross_attn_kernel<<<H * B, 256, 0, s>>>(part, ks, bias, xk, xv, H, B, T, beam, out);
+        return;
+    }
+    const int W = B / beam;
+    const unsigned grid = (unsigned)(((W * H + 7) / 8) * 8 * XCH);
+    switch (beam) {
+        case 1: dec_xattn_chunk_kernel<1><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out); break;
+        case 2: dec_xattn_chunk_kernel<2><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out); break;
+        case 3:
+        case 4: dec_xattn_chunk_kernel<4><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out); break;
+        case 5: dec_xattn_chunk_kernel<5><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out); break;
+        default: dec_xattn_chunk_kernel<8><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out); break;
+    }
 }
 
 void launch_dec_resid_ln(const float* part, int ks, int B, int D, const float* bias, float* x, const float* g,

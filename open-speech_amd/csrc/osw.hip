@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -34,8 +35,8 @@ uint64_t hash_stream_key(uint64_t, int64_t);
 void launch_dec_embed(const h16*, const float*, const int*, const int*, int, int, int, float*, hipStream_t);
 void launch_dec_self_attn(const float*, int, const float*, h16*, h16*, const int*, int, int, int, h16*, const int*,
                           hipStream_t);
-void launch_dec_cross_attn(const float*, int, const float*, const h16*, const h16*, int, int, int, int, h16*,
-                           hipStream_t);
+void launch_dec_cross_attn(const float*, int, const float*, const h16*, const h16*, int, int, int, int, h16*, float*,
+                           int*, hipStream_t);
 void launch_dec_resid_ln(const float*, int, int, int, const float*, float*, const float*, const float*, h16*,
                          const h16*, const float*, const int*, const int*, int, hipStream_t);
 void launch_dec_reduce_gelu(const float*, int, int, int, const float*, h16*, hipStream_t);
@@ -115,6 +116,8 @@ struct osw_ctx {
     int C1 = 0;   // conv1 input channels padded to a multiple of 64
     std::vector<void*> owned;
     std::map<std::string, Tensor> w;
+    std::shared_ptr<void> arena;  // weight arena, shared with sibling contexts (osw_create_sibling)
+    bool sibling = false;         // weights belong to another context: read-only here
     bool finalized = false;
 
     // mel constants
@@ -157,6 +160,8 @@ struct osw_ctx {
     void* bcand = nullptr;     // beam: [R][SEL_SPLIT][2*beam] candidates
     int* done_host = nullptr;  // pinned
     float* part = nullptr;     // split-K partial slabs of the decoder GEMMs
+    float* xws = nullptr;      // cross-attention per-chunk partials [R][H][XCHUNKS][XPART]
+    int* xticket = nullptr;    // cross-attention arrival tickets [B][H] (zero between launches)
     int64_t part_floats = 0;
 
     // decode-step graph (CH steps per replay), re-captured when its key changes
@@ -296,7 +301,15 @@ void build_weight_table(osw_ctx* c) {
     // one arena, every tensor 256-B aligned
     size_t total = 0;
     for (auto& kv : c->w) total += ((size_t)kv.second.numel * (kv.second.f16 ? 2 : 4) + 255) & ~(size_t)255;
-    char* arena = dalloc<char>(total, c->owned);
+    void* ap = nullptr;
+    if (hipMalloc(&ap, total) != hipSuccess)
+        throw OswError(OSW_ENOMEM, "hipMalloc " + std::to_string(total) + " B (weights) failed");
+    const int dev = c->device;
+    c->arena = std::shared_ptr<void>(ap, [dev](void* p) {
+        (void)hipSetDevice(dev);
+        (void)hipFree(p);
+    });
+    char* arena = (char*)ap;
     HIPCHK(hipMemsetAsync(arena, 0, total, c->stream));
     size_t off = 0;
     for (auto& kv : c->w) {
@@ -412,6 +425,9 @@ void setup_workspace(osw_ctx* c) {
     c->btok = dalloc<int>(B * d.n_text_ctx, o);
     c->bwin = dalloc<BeamWin>(B, o);
     c->bcand = dalloc<char>((size_t)R * beam_cand_bytes(MAX_BEAM), o);
+    c->xws = dalloc<float>(R * d.n_text_head * XCHUNKS * XPART, o);
+    c->xticket = dalloc<int>(B * d.n_text_head, o);
+    HIPCHK(hipMemset(c->xticket, 0, (size_t)B * d.n_text_head * sizeof(int)));
     {
         const int64_t Bm = std::min<int64_t>(R, 64);
         const int64_t shapes[][2] = {{3 * Dd, Dd}, {Dd, Dd}, {4 * Dd, Dd}, {Dd, 4 * Dd}, {d.n_vocab, Dd}};
@@ -567,7 +583,8 @@ void decoder_step(osw_ctx* c, int nb, int beam) {
         {
             Timed t(c, CL_XATTN, 2.0 * nb * H * (double)T_ENC * 64 * 2);
             launch_dec_cross_attn(c->part, ks, WF(c, p + ".xq.b"), c->XKV + (2 * l) * xkv_which,
-                                  c->XKV + (2 * l + 1) * xkv_which, nb, H, T_ENC, beam, c->dattn, c->stream);
+                                  c->XKV + (2 * l + 1) * xkv_which, nb, H, T_ENC, beam, c->dattn, c->xws,
+                                  c->xticket, c->stream);
         }
         ks = partial(c->dattn, D, WH(c, p + ".xo.w"), D, D);
         launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".xo.b"), c->xd, WF(c, p + ".ln3.g"), WF(c, p + ".ln3.b"),
@@ -862,6 +879,39 @@ int osw_create(const osw_dims* dims, int32_t device, int32_t max_batch, osw_ctx*
     return rc;
 }
 
+int osw_create_sibling(osw_ctx* parent, int32_t max_batch, osw_ctx** out) {
+    osw_ctx* c = nullptr;
+    int rc = guard([&] {
+        REQUIRE(parent && out, "null argument");
+        REQUIRE(max_batch >= 1 && max_batch <= 1024, "max_batch out of range");
+        std::lock_guard<std::mutex> lk(parent->mu);
+        REQUIRE(parent->finalized, "parent context weights not finalized");
+        c = new osw_ctx();
+        c->device = parent->device;
+        c->d = parent->d;
+        c->B = max_batch;
+        c->R = max_batch * 5;
+        c->C1 = parent->C1;
+        c->use_graph = parent->use_graph;
+        HIPCHK(hipSetDevice(c->device));
+        HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        c->w = parent->w;          // same device pointers
+        c->arena = parent->arena;  // keeps the weights alive past the parent's destroy
+        c->sibling = true;
+        c->finalized = true;
+        setup_mel(c);
+        setup_workspace(c);
+        HIPCHK(hipStreamSynchronize(c->stream));
+        *out = c;
+    });
+    if (rc != OSW_OK && c) {
+        for (void* p : c->owned) (void)hipFree(p);
+        if (c->stream) (void)hipStreamDestroy(c->stream);
+        delete c;
+    }
+    return rc;
+}
+
 int osw_destroy(osw_ctx* c) {
     if (!c) return OSW_OK;
     return guard([&] {
@@ -875,6 +925,7 @@ int osw_destroy(osw_ctx* c) {
             for (void* p : c->owned) (void)hipFree(p);
             if (c->done_host) (void)hipHostFree(c->done_host);
             (void)hipStreamDestroy(c->stream);
+            c->arena.reset();
         }
         delete c;
     });
@@ -884,6 +935,7 @@ int osw_set_weight(osw_ctx* c, const char* name, const void* host, int64_t nbyte
     return guard([&] {
         REQUIRE(c && name && host, "null argument");
         std::lock_guard<std::mutex> lk(c->mu);
+        REQUIRE(!c->sibling, "sibling contexts share their parent's weights (read-only)");
         HIPCHK(hipSetDevice(c->device));
         Tensor& t = W(c, name);
         const std::string nm(name);
@@ -909,6 +961,7 @@ int osw_init_weight_uniform(osw_ctx* c, const char* name, uint64_t seed, int64_t
     return guard([&] {
         REQUIRE(c && name, "null argument");
         std::lock_guard<std::mutex> lk(c->mu);
+        REQUIRE(!c->sibling, "sibling contexts share their parent's weights (read-only)");
         HIPCHK(hipSetDevice(c->device));
         Tensor& t = W(c, name);
         REQUIRE(!(std::string(name) == "enc.conv1.w" && c->C1 != c->d.n_mels),

@@ -6,8 +6,18 @@ PCM arrives at rank 0 and is scattered, the token ids are gathered back — and 
 run as RCCL collectives over xGMI when the backend is "nccl" (gloo on CPU for the
 tests).  int16 PCM travels viewed as int32 (RCCL has no int16 type; the bytes are
 unchanged).  No collective touches the compute path itself.
+
+Lanes: on a GPU rank the transcriber may drive several contexts that share one
+weight copy (``WhisperEngine.sibling``), each from its own host thread and HIP
+stream.  ``run_steps`` then overlaps consecutive steps: while lane 0 decodes step
+k (HBM- and launch-latency-bound), lane 1 runs step k+1's log-mel and encoder
+(MFMA-bound).  Collectives stay on the calling thread, in step order on every
+rank, so the RCCL call sequence is identical across ranks.
 """
 from __future__ import annotations
+
+from collections import deque
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -16,7 +26,7 @@ N_SAMPLES = 480000
 
 class DataParallelTranscriber:
     def __init__(self, engine, cfg, dist=None, device=None, clips_per_rank: int = 64, n_samples: int = N_SAMPLES,
-                 ctx: int = 448):
+                 ctx: int = 448, lanes: int = 1):
         import torch
 
         self.torch = torch
@@ -26,24 +36,35 @@ class DataParallelTranscriber:
         self.device = device if device is not None else torch.device("cpu")
         self.B, self.S, self.ctx = clips_per_rank, n_samples, ctx
         assert n_samples % 2 == 0, "int16 PCM travels as int32 pairs"
-        self.shard = torch.empty((self.B, self.S), dtype=torch.int16, device=self.device)
+        self.lanes = [engine] + [engine.sibling() for _ in range(max(1, lanes) - 1)]
+        # one shard buffer more than lanes: step k's buffer is free once step k - lanes - 1 is done
+        self.shards = [torch.empty((self.B, self.S), dtype=torch.int16, device=self.device)
+                       for _ in range(len(self.lanes) + 1)]
+        self.shard = self.shards[0]
         self.tok = torch.empty((self.B, ctx + 1), dtype=torch.int32, device=self.device)
         self.offsets = np.arange(self.B + 1, dtype=np.int64) * self.S
+        self.pool = ThreadPoolExecutor(len(self.lanes)) if len(self.lanes) > 1 else None
 
-    def scatter(self, all_pcm) -> None:
+    def scatter(self, all_pcm, slot: int = 0) -> None:
         """all_pcm: [world*B, S] int16 tensor on rank 0 (ignored elsewhere)."""
+        shard = self.shards[slot]
         if self.world == 1:
-            self.shard.copy_(all_pcm)
+            shard.copy_(all_pcm)
             return
         chunks = list(all_pcm.view(self.torch.int32).chunk(self.world)) if self.rank == 0 else None
-        self.dist.scatter(self.shard.view(self.torch.int32), chunks, src=0)
+        self.dist.scatter(shard.view(self.torch.int32), chunks, src=0)
 
-    def run_local(self):
+    def run_local(self, slot: int = 0, lane: int = 0):
+        eng, shard = self.lanes[lane], self.shards[slot]
         if self.device.type == "cuda":
-            self.torch.cuda.synchronize(self.device)
-            return self.engine.transcribe_batch(None, self.cfg, device_pcm=self.shard.data_ptr(),
-                                                offsets=self.offsets)
-        return self.engine.transcribe_batch(list(self.shard.numpy()), self.cfg)
+            return eng.transcribe_batch(None, self.cfg, device_pcm=shard.data_ptr(), offsets=self.offsets)
+        return eng.transcribe_batch(list(shard.numpy()), self.cfg)
+
+    def _sync(self) -> None:
+        # the scatter/copy ran on torch's current stream; the lanes use their own streams,
+        # so wait for this stream only (a device-wide sync would stall on the busy lanes)
+        if self.device.type == "cuda":
+            self.torch.cuda.current_stream(self.device).synchronize()
 
     def gather(self, outs):
         """Token ids of every clip on rank 0: list of lists in global clip order."""
@@ -65,5 +86,31 @@ class DataParallelTranscriber:
 
     def step(self, all_pcm=None):
         self.scatter(all_pcm)
+        self._sync()
         outs = self.run_local()
         return outs, self.gather(outs)
+
+    def run_steps(self, all_pcm, k: int):
+        """k steps (scatter -> transcribe -> gather each), consecutive steps overlapped on
+        the lanes.  Returns [(local outputs, gathered ids or None)] in step order."""
+        if self.pool is None:
+            return [self.step(all_pcm) for _ in range(k)]
+        nl, ns = len(self.lanes), len(self.shards)
+        res, inflight = [], deque()
+        for i in range(k):
+            if len(inflight) >= nl:  # every lane busy: finish the oldest step (frees its lane)
+                outs = inflight.popleft().result()
+                res.append((outs, self.gather(outs)))
+            self.scatter(all_pcm, i % ns)
+            self._sync()
+            inflight.append(self.pool.submit(self.run_local, i % ns, i % nl))
+        while inflight:
+            outs = inflight.popleft().result()
+            res.append((outs, self.gather(outs)))
+        return res
+
+    def close(self) -> None:
+        if self.pool is not None:
+            self.pool.shutdown(wait=True)
+        for e in self.lanes[1:]:
+            e.close()

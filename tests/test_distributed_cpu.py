@@ -23,6 +23,12 @@ class EchoEngine:
     def transcribe_batch(self, clips, cfg, device_pcm=None, offsets=None):
         return [_Out([int(c[0]), int(c[-1]), int(np.int64(c.astype(np.int64).sum()) % 50000)]) for c in clips]
 
+    def sibling(self):
+        return EchoEngine()
+
+    def close(self):
+        pass
+
 
 def _free_port():
     s = socket.socket()
@@ -32,7 +38,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, B, S, q):
+def _worker(rank, world, port, B, S, q, lanes=1, steps=1):
     import sys
     sys.path.insert(0, ROOT)
     import osw_path
@@ -42,25 +48,31 @@ def _worker(rank, world, port, B, S, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        dp = DataParallelTranscriber(EchoEngine(), None, dist=dist, clips_per_rank=B, n_samples=S, ctx=16)
+        dp = DataParallelTranscriber(EchoEngine(), None, dist=dist, clips_per_rank=B, n_samples=S, ctx=16,
+                                     lanes=lanes)
         allpcm = None
         if rank == 0:
             rng = np.random.default_rng(5)
             allpcm = torch.from_numpy(rng.integers(-30000, 30000, size=(world * B, S), dtype=np.int16))
-        outs, gathered = dp.step(allpcm)
+        if steps == 1 and lanes == 1:
+            outs, gathered = dp.step(allpcm)
+            res = [gathered]
+        else:
+            res = [g for _, g in dp.run_steps(allpcm, steps)]
+        dp.close()
         if rank == 0:
-            q.put(gathered)
+            q.put(res)
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_scatter_transcribe_gather_gloo(world):
+@pytest.mark.parametrize("world,lanes,steps", [(2, 1, 1), (2, 2, 3)])
+def test_scatter_transcribe_gather_gloo(world, lanes, steps):
     B, S = 3, 1000
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, B, S, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, B, S, q, lanes, steps)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=120)
@@ -70,7 +82,7 @@ def test_scatter_transcribe_gather_gloo(world):
     rng = np.random.default_rng(5)
     allpcm = rng.integers(-30000, 30000, size=(world * B, S), dtype=np.int16)
     want = EchoEngine().transcribe_batch(list(allpcm), None)
-    assert got == [w.tokens for w in want]
+    assert got == [[w.tokens for w in want]] * steps
 
 
 def test_single_rank_path():
@@ -81,3 +93,15 @@ def test_single_rank_path():
     pcm = torch.arange(20, dtype=torch.int16).reshape(2, 10)
     outs, g = dp.step(pcm)
     assert g == [[0, 9, 45], [10, 19, 145]]
+
+
+def test_single_rank_lanes_run_steps():
+    import osw_path
+    osw_path.load()
+    from open_speech_amd.distributed import DataParallelTranscriber
+    dp = DataParallelTranscriber(EchoEngine(), None, dist=None, clips_per_rank=2, n_samples=10, ctx=8, lanes=2)
+    assert len(dp.lanes) == 2 and len(dp.shards) == 3
+    pcm = torch.arange(20, dtype=torch.int16).reshape(2, 10)
+    res = dp.run_steps(pcm, 5)
+    dp.close()
+    assert [g for _, g in res] == [[[0, 9, 45], [10, 19, 145]]] * 5

@@ -214,3 +214,33 @@ def test_beam_batch_equals_single():
             assert abs(one.sum_logprob - together[i].sum_logprob) < 1e-3 * max(1.0, abs(one.sum_logprob))
     finally:
         eng.close()
+
+
+def test_sibling_shares_weights(tiny_engine):
+    """A sibling context (second lane on the same GPU) reads the parent's weights and
+    gives identical results, also while both run concurrently from two threads."""
+    import threading
+    d, eng, w = tiny_engine
+    sib = eng.sibling(max_batch=2)
+    try:
+        with pytest.raises(RuntimeError):
+            sib.set_weight("dec.lnpost.g", np.ones(d.n_text_state, np.float32))
+        sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+        cfg = DecodeConfig(suppress_tokens=sup, max_length=64)
+        clips = [synth.chirp_clip(31, 30.0), synth.chirp_clip(32, 11.0)]
+        ref = eng.transcribe_batch(clips, cfg)
+        got = {}
+
+        def run(name, e):
+            got[name] = [e.transcribe_batch(clips, cfg) for _ in range(3)]
+
+        th = [threading.Thread(target=run, args=(n, e)) for n, e in (("a", eng), ("b", sib))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        for outs in got["a"] + got["b"]:
+            for x, y in zip(outs, ref):
+                assert x.tokens == y.tokens and x.sum_logprob == y.sum_logprob
+    finally:
+        sib.close()

@@ -3,7 +3,9 @@
 ROCm 7 rocprofv3 --kernel-trace): top kernels by total time, in the same format as
 kstats.py.  Optional second argument: also write a kernel_stats-style CSV there.
 
-usage: kstats_db.py run_results.db [out.csv] [top_n]
+usage: kstats_db.py run_results.db [out.csv] [--gaps] [top_n]
+--gaps: also print the busy time vs. wall span of the kernel stream and the idle gap
+before each kernel class (launch boundaries; the stream is assumed to be serial).
 """
 import csv
 import sqlite3
@@ -13,6 +15,7 @@ from collections import defaultdict
 db = sys.argv[1]
 out_csv = sys.argv[2] if len(sys.argv) > 2 and sys.argv[2].endswith(".csv") else None
 n = int(sys.argv[-1]) if sys.argv[-1].isdigit() else 30
+gaps = "--gaps" in sys.argv
 c = sqlite3.connect(db)
 agg = defaultdict(lambda: [0, 0.0, float("inf"), 0.0])
 for name, dur in c.execute("select name, duration from kernels"):
@@ -32,3 +35,21 @@ if out_csv:
         w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs"])
         for name, (calls, s, mn, mx) in rows:
             w.writerow([name, calls, int(s), s / calls, 100 * s / tot, int(mn), int(mx)])
+if gaps:
+    ev = sorted(c.execute("select name, start, end from kernels"), key=lambda r: r[1])
+    busy = sum(e - s for _, s, e in ev)
+    gap_by = defaultdict(lambda: [0, 0.0])
+    big = 0.0
+    for (n0, s0, e0), (n1, s1, e1) in zip(ev, ev[1:]):
+        g = s1 - e0
+        if g > 200e3:  # > 200 us: host-side pause (sync, python), not a launch boundary
+            big += g
+            continue
+        gap_by[n1][0] += 1
+        gap_by[n1][1] += max(0, g)
+    span = ev[-1][2] - ev[0][1]
+    small = sum(v[1] for v in gap_by.values())
+    print(f"kernels {len(ev)}: busy {busy / 1e6:.2f} ms, span {span / 1e6:.2f} ms, "
+          f"boundary gaps {small / 1e6:.2f} ms ({small / max(1, len(ev)) / 1e3:.2f} us avg), host pauses {big / 1e6:.2f} ms")
+    for name, (k, g) in sorted(gap_by.items(), key=lambda kv: -kv[1][1])[:12]:
+        print(f"  gap before {name[:80]}: n={k} avg {g / k / 1e3:.2f} us")

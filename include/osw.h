@@ -122,6 +122,9 @@ int osw_create_sibling(osw_ctx* parent, int32_t max_batch, osw_ctx** out);
 
 /* Upload one canonical tensor (names and dtypes: open-speech_amd/weights.py). */
 int osw_set_weight(osw_ctx* ctx, const char* name, const void* host, int64_t nbytes);
+/* Read one tensor back as stored on the device (enc.conv1.w: the padded [De][3][C1]
+ * layout).  For tests and checkpoint round trips. */
+int osw_get_weight(osw_ctx* ctx, const char* name, void* host, int64_t nbytes);
 /* Device-side counter-hash init: x[i] = (2u-1)*scale + offset, u from splitmix64. */
 int osw_init_weight_uniform(osw_ctx* ctx, const char* name, uint64_t seed, int64_t stream,
                             float scale, float offset, int64_t zero_lo, int64_t zero_hi);

@@ -65,6 +65,7 @@ _SIGS = {
     "osw_destroy": (C.c_int, [C.c_void_p]),
     "osw_create_sibling": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_void_p)]),
     "osw_set_weight": (C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_int64]),
+    "osw_get_weight": (C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_int64]),
     "osw_init_weight_uniform": (C.c_int, [C.c_void_p, C.c_char_p, C.c_uint64, C.c_int64, C.c_float, C.c_float,
                                           C.c_int64, C.c_int64]),
     "osw_finalize": (C.c_int, [C.c_void_p]),

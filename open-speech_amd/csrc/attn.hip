@@ -127,8 +127,8 @@ __global__ __launch_bounds__(256, 2) void enc_attn_kernel(const h16* __restrict_
                     sc[qt][t][i] = v;
                     mx = fmaxf(mx, v);
                 }
-            mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            mx = fmaxf(mx, xor_lane<16>(mx));
+            mx = fmaxf(mx, xor_lane<32>(mx));
             const float mnew = fmaxf(mrun[qt], mx);
             const float alpha = exp2f(mrun[qt] - mnew);
             mrun[qt] = mnew;
@@ -187,8 +187,8 @@ __global__ __launch_bounds__(256, 2) void enc_attn_kernel(const h16* __restrict_
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
         float l = lrun[qt];
-        l += __shfl_xor(l, 16, 64);
-        l += __shfl_xor(l, 32, 64);
+        l += xor_lane<16>(l);
+        l += xor_lane<32>(l);
         const float inv = 1.0f / l;
         const int q = q0 + qt * 16 + li;
         if (q >= T) continue;

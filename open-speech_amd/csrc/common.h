@@ -25,19 +25,73 @@ __device__ __forceinline__ float ordered_to_float(int i) {
     return __int_as_float(i >= 0 ? i : (i ^ 0x7fffffff));
 }
 
+// erf(x) to |error| <= 1.5e-7 (Abramowitz & Stegun 7.1.26): one reciprocal, one exp,
+// five FMAs and no branches.  ocml's erff takes a divergent two-branch path that made
+// the GELU epilogue of the encoder fc1 GEMM ~30 % of that kernel's time; the result
+// is stored as fp16 (relative step 4.9e-4), far above this error.
+__device__ __forceinline__ float erf_fast(float x) {
+    const float ax = fabsf(x);
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.0f));
+    float y = fmaf(fmaf(fmaf(fmaf(1.061405429f, t, -1.453152027f), t, 1.421413741f), t, -0.284496736f), t,
+                   0.254829592f) * t;
+    y = 1.0f - y * __expf(-ax * ax);
+    return copysignf(y, x);
+}
+
 __device__ __forceinline__ float gelu_erf(float x) {
-    return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+    return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f));
+}
+
+// Lane exchange v[lane ^ O] without the LDS pipe: DPP for O <= 8 (quad_perm, half-row
+// mirror + quad reverse for 4, row rotate for 8), gfx950's v_permlane{16,32}_swap for
+// 16 / 32.  ds_bpermute (what __shfl_xor lowers to) with several permutes in flight
+// returned stale lanes when another queue's LDS-DMA kernels shared the CU (the decoder
+// of one context drifted while a second context encoded; DESIGN.md "Determinism"),
+// and DPP is also a few cycles instead of an LDS round trip.
+template <int V>
+using IC = std::integral_constant<int, V>;
+template <int O>
+__device__ __forceinline__ int xor_lane(int v) {
+    static_assert(O == 1 || O == 2 || O == 4 || O == 8 || O == 16 || O == 32, "xor distance");
+    if constexpr (O == 1) {
+        return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+    } else if constexpr (O == 2) {
+        return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+    } else if constexpr (O == 4) {
+        const int t = __builtin_amdgcn_update_dpp(0, v, 0x141, 0xf, 0xf, false);  // row_half_mirror: i -> 7-i
+        return __builtin_amdgcn_update_dpp(0, t, 0x1B, 0xf, 0xf, false);          // quad_perm [3,2,1,0]
+    } else if constexpr (O == 8) {
+        return __builtin_amdgcn_update_dpp(0, v, 0x128, 0xf, 0xf, false);  // row_ror:8 == xor 8 in a 16-lane row
+    } else if constexpr (O == 16) {
+        // (v, v) -> first = rows [0,0,2,2], second = rows [1,1,3,3]
+        const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+        return (int)((__lane_id() & 16) ? r[0] : r[1]);
+    } else {
+        // (v, v) -> first = halves [lo,lo], second = [hi,hi]
+        const auto r = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+        return (int)((__lane_id() & 32) ? r[0] : r[1]);
+    }
+}
+template <int O>
+__device__ __forceinline__ float xor_lane(float v) {
+    return __int_as_float(xor_lane<O>(__float_as_int(v)));
 }
 
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
+    v = fmaxf(v, xor_lane<32>(v));
+    v = fmaxf(v, xor_lane<16>(v));
+    v = fmaxf(v, xor_lane<8>(v));
+    v = fmaxf(v, xor_lane<4>(v));
+    v = fmaxf(v, xor_lane<2>(v));
+    return fmaxf(v, xor_lane<1>(v));
 }
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    v += xor_lane<32>(v);
+    v += xor_lane<16>(v);
+    v += xor_lane<8>(v);
+    v += xor_lane<4>(v);
+    v += xor_lane<2>(v);
+    return v + xor_lane<1>(v);
 }
 
 // GEMM epilogue selector (see gemm.hip)
@@ -68,6 +122,7 @@ void launch_gemm(const GemmArgs& g, hipStream_t s);
 void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s);  // 0 auto, 1 128-tile, 2 256-tile
 // M <= 64, K % 128 == 0; `part` needs skinny_ksplit(N,K)*M*N floats
 void launch_gemm_skinny(const GemmArgs& g, float* part, hipStream_t s);
+void launch_gemm_skinny_direct(const GemmArgs& g, hipStream_t s);  // ksplit 1, fused epilogue (F16 / F16_GELU)
 int skinny_ksplit(int N, int K);
 int tiled_ksplit(int M, int N, int K);
 void launch_gemm_tiled_partial(const GemmArgs& g, float* part, int ks, hipStream_t s);

@@ -9,6 +9,7 @@
 #include "decode.h"
 
 #include <climits>
+#include <cstdio>
 #include <cstdlib>
 
 namespace osw {
@@ -84,9 +85,9 @@ __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ 
             float d = 0.f;
 #pragma unroll
             for (int i = 0; i < 8; ++i) d = fmaf((float)kv[u][i], q[i], d);
-            d += __shfl_xor(d, 1, 64);
-            d += __shfl_xor(d, 2, 64);
-            d += __shfl_xor(d, 4, 64);
+            d += xor_lane<1>(d);
+            d += xor_lane<2>(d);
+            d += xor_lane<4>(d);
             const int key = base + u * 32 + w * 8 + kr;
             if (key < n_keys) {
                 if (c8 == 0) sc[key] = d;
@@ -213,12 +214,12 @@ __global__ __launch_bounds__(256) void dec_cross_attn_kernel(const float* __rest
 // workgroup, the whole chunk in one HBM round trip), then reduces the rows' q from
 // the q projection's split-K slabs while the loads land.  Per row it writes the
 // chunk max m, l = Σ exp(s - m) and the unnormalised Σ exp(s - m)·v to a workspace
-// and takes an arrival ticket; the last workgroup of the (window, head) merges the
-// 8 chunks in fixed chunk order, so the output does not depend on the batch size or
-// the dispatch order.  Small batches get 8x the workgroups of one-per-(row, head)
-// (B = 1: 160 instead of 20), and beam rows read each K/V chunk once, not per row.
-// Chunks of one (window, head) go to the same XCD (bid % 8), so the partials and
-// the ticket stay in one L2.
+// and dec_xattn_merge_kernel merges the 8 chunks of each (row, head) in fixed chunk
+// order, so the output does not depend on the batch size or the dispatch order.
+// (A last-arriver merge inside this kernel needs agent-scope release fences, which
+// write back the XCD's L2 on gfx950: measured 7x slower at 64 windows.)  Small
+// batches get 8x the workgroups of one-per-(row, head) (B = 1: 160 instead of 20),
+// and beam rows read each K/V chunk once instead of once per row.
 // Lane map: kg = tid >> 3 (32 key groups), c = tid & 7 (dims 8c..8c+7); the lane
 // holds keys u*32 + kg (u = 0..5) of the chunk for both scores and P·V.
 constexpr int XCH = XCHUNKS, XKEYS = 192, XU = XKEYS / 32;
@@ -228,16 +229,14 @@ template <int NB>
 __global__ __launch_bounds__(256) void dec_xattn_chunk_kernel(const float* __restrict__ part, int ks,
                                                               const float* __restrict__ bias,
                                                               const h16* __restrict__ xk, const h16* __restrict__ xv,
-                                                              int H, int W, int T, int beam, float* __restrict__ ws,
-                                                              int* __restrict__ ticket, h16* __restrict__ out) {
+                                                              int H, int W, int T, int beam, float* __restrict__ ws) {
     __shared__ float red[4][NB][HD];
     __shared__ float rm[4][NB], rl[4][NB];
     __shared__ float qsh[NB][HD];
-    __shared__ int is_last;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, kg = tid >> 3, c = tid & 7;
     const int bid = blockIdx.x;
     const int chunk = (bid >> 3) & 7;
-    const int p = (bid & 7) + 8 * (bid >> 6);  // (window, head) pair; its 8 chunks share bid % 8
+    const int p = (bid & 7) + 8 * (bid >> 6);  // (window, head) pair; its 8 chunks share one XCD (bid % 8)
     if (p >= W * H) return;
     const int h = p % H, w = p / H;
     const int D = H * HD;
@@ -289,9 +288,9 @@ __global__ __launch_bounds__(256) void dec_xattn_chunk_kernel(const float* __res
             float d = 0.f;
 #pragma unroll
             for (int i = 0; i < 8; ++i) d = fmaf((float)kf[u][i], q[i], d);
-            d += __shfl_xor(d, 1, 64);
-            d += __shfl_xor(d, 2, 64);
-            d += __shfl_xor(d, 4, 64);
+            d += xor_lane<1>(d);
+            d += xor_lane<2>(d);
+            d += xor_lane<4>(d);
             sc[k][u] = d;
             if (u * 32 + kg < nk) mx[k] = fmaxf(mx[k], d);
         }
@@ -320,9 +319,9 @@ __global__ __launch_bounds__(256) void dec_xattn_chunk_kernel(const float* __res
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             float a = acc[k][e];
-            a += __shfl_xor(a, 8, 64);
-            a += __shfl_xor(a, 16, 64);
-            a += __shfl_xor(a, 32, 64);
+            a += xor_lane<8>(a);
+            a += xor_lane<16>(a);
+            a += xor_lane<32>(a);
             acc[k][e] = a;
         }
         float l = c == 0 ? ls[k] : 0.f;
@@ -339,41 +338,40 @@ __global__ __launch_bounds__(256) void dec_xattn_chunk_kernel(const float* __res
         for (int k = 0; k < NB; ++k) {
             if (k >= beam) break;
             float* dst = ws + (((int64_t)(r0 + k) * H + h) * XCH + chunk) * XPART;
-            dst[4 + lane] = (red[0][k][lane] + red[1][k][lane]) + (red[2][k][lane] + red[3][k][lane]);
+            const float a = (red[0][k][lane] + red[1][k][lane]) + (red[2][k][lane] + red[3][k][lane]);
+            const float l = (rl[0][k] + rl[1][k]) + (rl[2][k] + rl[3][k]);
+            dst[4 + lane] = a;
             if (lane == 0) {
                 dst[0] = mx[k];
-                dst[1] = (rl[0][k] + rl[1][k]) + (rl[2][k] + rl[3][k]);
+                dst[1] = l;
             }
         }
     }
-    __threadfence();
-    __syncthreads();
-    if (tid == 0) {
-        const int old = atomicAdd(&ticket[p], 1);
-        is_last = old == XCH - 1;
-        if (old == XCH - 1) ticket[p] = 0;  // every chunk has arrived: reset for the next launch
-    }
-    __syncthreads();
-    if (!is_last) return;
-    __threadfence();
-    for (int k = wv; k < beam; k += 4) {
-        const float* src = ws + ((int64_t)(r0 + k) * H + h) * XCH * XPART;
-        float mm[XCH];
-        float M = -INFINITY;
+}
+
+// grid ceil(rows*H/4), 256 threads: lane d of wave (row, head) merges the XCH chunk
+// partials in chunk order: out = Σ e^(m_s - M) acc_s / Σ e^(m_s - M) l_s, fp16.
+__global__ __launch_bounds__(256) void dec_xattn_merge_kernel(const float* __restrict__ ws, int rows, int H,
+                                                              h16* __restrict__ out) {
+    const int pr = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (pr >= rows * H) return;
+    const float* src = ws + (int64_t)pr * XCH * XPART;
+    float mm[XCH];
+    float M = -INFINITY;
 #pragma unroll
-        for (int s = 0; s < XCH; ++s) {
-            mm[s] = __hip_atomic_load(src + s * XPART, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            M = fmaxf(M, mm[s]);
-        }
-        float L = 0.f, O = 0.f;
-#pragma unroll
-        for (int s = 0; s < XCH; ++s) {
-            const float e = __expf(mm[s] - M);
-            L = fmaf(__hip_atomic_load(src + s * XPART + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), e, L);
-            O = fmaf(__hip_atomic_load(src + s * XPART + 4 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), e, O);
-        }
-        out[(int64_t)(r0 + k) * D + h * HD + lane] = (h16)(O / L);
+    for (int s = 0; s < XCH; ++s) {
+        mm[s] = src[s * XPART];
+        M = fmaxf(M, mm[s]);
     }
+    float L = 0.f, O = 0.f;
+#pragma unroll
+    for (int s = 0; s < XCH; ++s) {
+        const float e = __expf(mm[s] - M);
+        L = fmaf(src[s * XPART + 1], e, L);
+        O = fmaf(src[s * XPART + 4 + lane], e, O);
+    }
+    const int r = pr / H, h = pr % H;
+    out[(int64_t)r * H * HD + h * HD + lane] = (h16)(O / L);
 }
 
 // grid B, 1024 threads: x[b] += bias + Σ split-K partials (residual stream, fp32),
@@ -561,16 +559,15 @@ __global__ __launch_bounds__(256) void select_partial_kernel(const float* __rest
             a_text = amax(a_text, ArgMax{xv, v});
         }
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        float m2 = __shfl_xor(m_all, o, 64), s2 = __shfl_xor(s_all, o, 64);
-        lse_merge(m_all, s_all, m2, s2);
-        m2 = __shfl_xor(m_ts, o, 64);
-        s2 = __shfl_xor(s_ts, o, 64);
-        lse_merge(m_ts, s_ts, m2, s2);
-        a_all = amax(a_all, ArgMax{__shfl_xor(a_all.v, o, 64), __shfl_xor(a_all.i, o, 64)});
-        a_text = amax(a_text, ArgMax{__shfl_xor(a_text.v, o, 64), __shfl_xor(a_text.i, o, 64)});
-        a_ts = amax(a_ts, ArgMax{__shfl_xor(a_ts.v, o, 64), __shfl_xor(a_ts.i, o, 64)});
-    }
+    auto merge = [&](auto o) {
+        constexpr int O = decltype(o)::value;
+        lse_merge(m_all, s_all, xor_lane<O>(m_all), xor_lane<O>(s_all));
+        lse_merge(m_ts, s_ts, xor_lane<O>(m_ts), xor_lane<O>(s_ts));
+        a_all = amax(a_all, ArgMax{xor_lane<O>(a_all.v), xor_lane<O>(a_all.i)});
+        a_text = amax(a_text, ArgMax{xor_lane<O>(a_text.v), xor_lane<O>(a_text.i)});
+        a_ts = amax(a_ts, ArgMax{xor_lane<O>(a_ts.v), xor_lane<O>(a_ts.i)});
+    };
+    merge(IC<32>{}), merge(IC<16>{}), merge(IC<8>{}), merge(IC<4>{}), merge(IC<2>{}), merge(IC<1>{});
     __shared__ SelPart wp[4];
     const int w = tid >> 6;
     if ((tid & 63) == 0) wp[w] = SelPart{m_all, s_all, m_ts, s_ts, a_all.v, a_text.v, a_ts.v, a_all.i, a_text.i, a_ts.i};
@@ -678,7 +675,11 @@ struct BeamCand {
 
 // block-wide argmax (value desc, index asc) of one candidate per thread, 256 threads
 __device__ __forceinline__ ArgMax block_amax(ArgMax a, ArgMax* red) {
-    for (int o = 32; o > 0; o >>= 1) a = amax(a, ArgMax{__shfl_xor(a.v, o, 64), __shfl_xor(a.i, o, 64)});
+    auto step = [&](auto o) {
+        constexpr int O = decltype(o)::value;
+        a = amax(a, ArgMax{xor_lane<O>(a.v), xor_lane<O>(a.i)});
+    };
+    step(IC<32>{}), step(IC<16>{}), step(IC<8>{}), step(IC<4>{}), step(IC<2>{}), step(IC<1>{});
     const int w = threadIdx.x >> 6;
     __syncthreads();
     if ((threadIdx.x & 63) == 0) red[w] = a;
@@ -936,7 +937,7 @@ void launch_dec_self_attn(const float* part, int ks, const float* bias, h16* kc,
 }
 
 void launch_dec_cross_attn(const float* part, int ks, const float* bias, const h16* xk, const h16* xv, int B, int H,
-                           int T, int beam, h16* out, float* ws, int* ticket, hipStream_t s) {
+                           int T, int beam, h16* out, float* ws, hipStream_t s) {
     static const bool legacy = std::getenv("OSW_XATTN_LEGACY") != nullptr;  // A/B switch: one workgroup per (row, head)
     if (legacy || !ws) {
         dec_cross_attn_kernel<<<H * B, 256, 0, s>>>(part, ks, bias, xk, xv, H, B, T, beam, out);
@@ -945,13 +946,14 @@ void launch_dec_cross_attn(const float* part, int ks, const float* bias, const h
     const int W = B / beam;
     const unsigned grid = (unsigned)(((W * H + 7) / 8) * 8 * XCH);
     switch (beam) {
-        case 1: dec_xattn_chunk_kernel<1><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out); break;
-        case 2: dec_xattn_chunk_kernel<2><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out); break;
+        case 1: dec_xattn_chunk_kernel<1><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws); break;
+        case 2: dec_xattn_chunk_kernel<2><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws); break;
         case 3:
-        case 4: dec_xattn_chunk_kernel<4><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out); break;
-        case 5: dec_xattn_chunk_kernel<5><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out); break;
-        default: dec_xattn_chunk_kernel<8><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out); break;
+        case 4: dec_xattn_chunk_kernel<4><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws); break;
+        case 5: dec_xattn_chunk_kernel<5><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws); break;
+        default: dec_xattn_chunk_kernel<8><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws); break;
     }
+    dec_xattn_merge_kernel<<<(unsigned)((B * H + 3) / 4), 256, 0, s>>>(ws, B, H, out);
 }
 
 void launch_dec_resid_ln(const float* part, int ks, int B, int D, const float* bias, float* x, const float* g,

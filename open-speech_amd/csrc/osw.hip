@@ -36,7 +36,7 @@ void launch_dec_embed(const h16*, const float*, const int*, const int*, int, int
 void launch_dec_self_attn(const float*, int, const float*, h16*, h16*, const int*, int, int, int, h16*, const int*,
                           hipStream_t);
 void launch_dec_cross_attn(const float*, int, const float*, const h16*, const h16*, int, int, int, int, h16*, float*,
-                           int*, hipStream_t);
+                           hipStream_t);
 void launch_dec_resid_ln(const float*, int, int, int, const float*, float*, const float*, const float*, h16*,
                          const h16*, const float*, const int*, const int*, int, hipStream_t);
 void launch_dec_reduce_gelu(const float*, int, int, int, const float*, h16*, hipStream_t);
@@ -161,7 +161,6 @@ struct osw_ctx {
     int* done_host = nullptr;  // pinned
     float* part = nullptr;     // split-K partial slabs of the decoder GEMMs
     float* xws = nullptr;      // cross-attention per-chunk partials [R][H][XCHUNKS][XPART]
-    int* xticket = nullptr;    // cross-attention arrival tickets [B][H] (zero between launches)
     int64_t part_floats = 0;
 
     // decode-step graph (CH steps per replay), re-captured when its key changes
@@ -426,8 +425,6 @@ void setup_workspace(osw_ctx* c) {
     c->bwin = dalloc<BeamWin>(B, o);
     c->bcand = dalloc<char>((size_t)R * beam_cand_bytes(MAX_BEAM), o);
     c->xws = dalloc<float>(R * d.n_text_head * XCHUNKS * XPART, o);
-    c->xticket = dalloc<int>(B * d.n_text_head, o);
-    HIPCHK(hipMemset(c->xticket, 0, (size_t)B * d.n_text_head * sizeof(int)));
     {
         const int64_t Bm = std::min<int64_t>(R, 64);
         const int64_t shapes[][2] = {{3 * Dd, Dd}, {Dd, Dd}, {4 * Dd, Dd}, {Dd, 4 * Dd}, {d.n_vocab, Dd}};
@@ -584,13 +581,20 @@ void decoder_step(osw_ctx* c, int nb, int beam) {
             Timed t(c, CL_XATTN, 2.0 * nb * H * (double)T_ENC * 64 * 2);
             launch_dec_cross_attn(c->part, ks, WF(c, p + ".xq.b"), c->XKV + (2 * l) * xkv_which,
                                   c->XKV + (2 * l + 1) * xkv_which, nb, H, T_ENC, beam, c->dattn, c->xws,
-                                  c->xticket, c->stream);
+                                  c->stream);
         }
         ks = partial(c->dattn, D, WH(c, p + ".xo.w"), D, D);
         launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".xo.b"), c->xd, WF(c, p + ".ln3.g"), WF(c, p + ".ln3.b"),
                             c->xdn, nullptr, nullptr, nullptr, nullptr, ctx, c->stream);
-        ks = partial(c->xdn, D, WH(c, p + ".fc1.w"), 4 * D, D);
-        launch_dec_reduce_gelu(c->part, ks, nb, 4 * D, WF(c, p + ".fc1.b"), c->dh, c->stream);
+        static const int fc1_direct = std::getenv("OSW_FC1_SPLIT") ? 0 : 1;  // A/B switch
+        if (fc1_direct && nb <= 64 && D % 128 == 0) {
+            // whole-K workgroups with the bias + GELU epilogue: no slabs, no reduce kernel
+            launch_gemm_skinny_direct(gemm_plain(c->xdn, D, WH(c, p + ".fc1.w"), WF(c, p + ".fc1.b"), nb, 4 * D, D,
+                                                 c->dh, 4 * D, EPI_F16_GELU), c->stream);
+        } else {
+            ks = partial(c->xdn, D, WH(c, p + ".fc1.w"), 4 * D, D);
+            launch_dec_reduce_gelu(c->part, ks, nb, 4 * D, WF(c, p + ".fc1.b"), c->dh, c->stream);
+        }
         ks = partial(c->dh, 4 * D, WH(c, p + ".fc2.w"), D, 4 * D);
         const std::string nx = l + 1 < L ? "dec.l" + std::to_string(l + 1) + ".ln1" : std::string("dec.lnpost");
         launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".fc2.b"), c->xd, WF(c, nx + ".g"), WF(c, nx + ".b"), c->xdn,
@@ -953,6 +957,18 @@ int osw_set_weight(osw_ctx* c, const char* name, const void* host, int64_t nbyte
             HIPCHK(hipMemcpy(t.ptr, host, nbytes, hipMemcpyHostToDevice));
         }
         t.set = true;
+    });
+}
+
+int osw_get_weight(osw_ctx* c, const char* name, void* host, int64_t nbytes) {
+    return guard([&] {
+        REQUIRE(c && name && host, "null argument");
+        std::lock_guard<std::mutex> lk(c->mu);
+        HIPCHK(hipSetDevice(c->device));
+        Tensor& t = W(c, name);
+        REQUIRE(nbytes == t.numel * (t.f16 ? 2 : 4), std::string("tensor ") + name + ": wrong byte count");
+        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipMemcpy(host, t.ptr, nbytes, hipMemcpyDeviceToHost));
     });
 }
 

@@ -158,6 +158,9 @@ int osw_encoder_layer_debug(osw_ctx* ctx, int32_t layer, const float* x, float* 
 int osw_debug_gemm(osw_ctx* ctx, int32_t M, int32_t N, int32_t K, int32_t variant, const void* A, const void* W,
                    float* C, int32_t iters, float* ms);
 
+/* 0 off; 1 per-stage HIP-event timers (decode steps stay in their hipGraph, so only
+ * mel / encoder stages are timed); 2 also launches the decode steps eagerly so the
+ * cross-attention timers see them.  Resets the counters. */
 int osw_set_profiling(osw_ctx* ctx, int32_t enable);
 int osw_get_profile(osw_ctx* ctx, osw_profile* out);
 /* Device stream used by the context (hipStream_t as void*). */

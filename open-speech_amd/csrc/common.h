@@ -122,7 +122,6 @@ void launch_gemm(const GemmArgs& g, hipStream_t s);
 void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s);  // 0 auto, 1 128-tile, 2 256-tile
 // M <= 64, K % 128 == 0; `part` needs skinny_ksplit(N,K)*M*N floats
 void launch_gemm_skinny(const GemmArgs& g, float* part, hipStream_t s);
-void launch_gemm_skinny_direct(const GemmArgs& g, hipStream_t s);  // ksplit 1, fused epilogue (F16 / F16_GELU)
 int skinny_ksplit(int N, int K);
 int tiled_ksplit(int M, int N, int K);
 void launch_gemm_tiled_partial(const GemmArgs& g, float* part, int ks, hipStream_t s);

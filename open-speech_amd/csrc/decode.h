@@ -35,9 +35,9 @@ constexpr int XPART = 72;     // floats per (decoder row, head, key chunk) cross
 constexpr int XCHUNKS = 8;    // fixed key chunks per (window, head) in cross-attention
 constexpr int SEL_SPLIT = 16;  // vocabulary slices per row in the selection kernels
 
-void launch_select(const float* logits, int rows, const int* pos, const SelParams& P, const int* prompt,
+void launch_select(const float* logits, int rows, int* pos, const SelParams& P, const int* prompt,
                    const unsigned* supmask, SelState* st, int* cur_tok, int* tokens, int max_tokens, void* sel_parts,
-                   hipStream_t s);
+                   int* arrive, bool bump, hipStream_t s);
 void launch_beam(const float* logits, int windows, const int* pos, const SelParams& P, const unsigned* supmask,
                  SelState* st, const void* sel_parts, void* cand, int* seq, int* anc, int ctx, BeamWin* bw,
                  int* best_tok, int* cur_tok, int max_tokens, hipStream_t s);

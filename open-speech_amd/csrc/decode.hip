@@ -214,10 +214,11 @@ __global__ __launch_bounds__(256) void dec_cross_attn_kernel(const float* __rest
 // workgroup, the whole chunk in one HBM round trip), then reduces the rows' q from
 // the q projection's split-K slabs while the loads land.  Per row it writes the
 // chunk max m, l = Σ exp(s - m) and the unnormalised Σ exp(s - m)·v to a workspace
-// and dec_xattn_merge_kernel merges the 8 chunks of each (row, head) in fixed chunk
-// order, so the output does not depend on the batch size or the dispatch order.
-// (A last-arriver merge inside this kernel needs agent-scope release fences, which
-// write back the XCD's L2 on gfx950: measured 7x slower at 64 windows.)  Small
+// with device-scope stores (they write through the XCD's L2; a release fence would
+// write back the whole L2 instead, measured 7x slower at 64 windows) and takes an
+// arrival ticket; the last of the 8 chunk workgroups of a (window, head) merges them
+// in fixed chunk order, so the output does not depend on the batch size, dispatch
+// order or XCD placement, and no separate merge launch is needed.  Small
 // batches get 8x the workgroups of one-per-(row, head) (B = 1: 160 instead of 20),
 // and beam rows read each K/V chunk once instead of once per row.
 // Lane map: kg = tid >> 3 (32 key groups), c = tid & 7 (dims 8c..8c+7); the lane
@@ -229,7 +230,8 @@ template <int NB>
 __global__ __launch_bounds__(256) void dec_xattn_chunk_kernel(const float* __restrict__ part, int ks,
                                                               const float* __restrict__ bias,
                                                               const h16* __restrict__ xk, const h16* __restrict__ xv,
-                                                              int H, int W, int T, int beam, float* __restrict__ ws) {
+                                                              int H, int W, int T, int beam, float* __restrict__ ws,
+                                                              int* __restrict__ ticket, h16* __restrict__ out) {
     __shared__ float red[4][NB][HD];
     __shared__ float rm[4][NB], rl[4][NB];
     __shared__ float qsh[NB][HD];
@@ -333,45 +335,47 @@ __global__ __launch_bounds__(256) void dec_xattn_chunk_kernel(const float* __res
         }
     }
     __syncthreads();
-    if (wv == 0) {
+    if (wv != 0) return;
+    // publish this chunk's partials with device-scope (write-through) stores, wait for
+    // them, then take the (window, head) arrival ticket: the 8th arriver merges
 #pragma unroll
-        for (int k = 0; k < NB; ++k) {
-            if (k >= beam) break;
-            float* dst = ws + (((int64_t)(r0 + k) * H + h) * XCH + chunk) * XPART;
-            const float a = (red[0][k][lane] + red[1][k][lane]) + (red[2][k][lane] + red[3][k][lane]);
-            const float l = (rl[0][k] + rl[1][k]) + (rl[2][k] + rl[3][k]);
-            dst[4 + lane] = a;
-            if (lane == 0) {
-                dst[0] = mx[k];
-                dst[1] = l;
-            }
+    for (int k = 0; k < NB; ++k) {
+        if (k >= beam) break;
+        float* dst = ws + (((int64_t)(r0 + k) * H + h) * XCH + chunk) * XPART;
+        const float a = (red[0][k][lane] + red[1][k][lane]) + (red[2][k][lane] + red[3][k][lane]);
+        const float l = (rl[0][k] + rl[1][k]) + (rl[2][k] + rl[3][k]);
+        __hip_atomic_store(dst + 4 + lane, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) {
+            __hip_atomic_store(dst, mx[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(dst + 1, l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-}
-
-// grid ceil(rows*H/4), 256 threads: lane d of wave (row, head) merges the XCH chunk
-// partials in chunk order: out = Σ e^(m_s - M) acc_s / Σ e^(m_s - M) l_s, fp16.
-__global__ __launch_bounds__(256) void dec_xattn_merge_kernel(const float* __restrict__ ws, int rows, int H,
-                                                              h16* __restrict__ out) {
-    const int pr = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (pr >= rows * H) return;
-    const float* src = ws + (int64_t)pr * XCH * XPART;
-    float mm[XCH];
-    float M = -INFINITY;
+    __builtin_amdgcn_s_waitcnt(0);  // the stores above are complete at device scope
+    int old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(ticket + p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old != XCH - 1) return;
+    if (lane == 0) __hip_atomic_store(ticket + p, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+    // merge in fixed chunk order: out = Σ e^(m_s - M) acc_s / Σ e^(m_s - M) l_s (device-scope
+    // loads: the other chunks' partials may come from another XCD's writes)
+    for (int k = 0; k < beam; ++k) {
+        const float* src = ws + ((int64_t)(r0 + k) * H + h) * XCH * XPART;
+        float mm[XCH];
+        float M = -INFINITY;
 #pragma unroll
-    for (int s = 0; s < XCH; ++s) {
-        mm[s] = src[s * XPART];
-        M = fmaxf(M, mm[s]);
-    }
-    float L = 0.f, O = 0.f;
+        for (int q = 0; q < XCH; ++q) {
+            mm[q] = __hip_atomic_load(src + q * XPART, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            M = fmaxf(M, mm[q]);
+        }
+        float L = 0.f, O = 0.f;
 #pragma unroll
-    for (int s = 0; s < XCH; ++s) {
-        const float e = __expf(mm[s] - M);
-        L = fmaf(src[s * XPART + 1], e, L);
-        O = fmaf(src[s * XPART + 4 + lane], e, O);
+        for (int q = 0; q < XCH; ++q) {
+            const float e = __expf(mm[q] - M);
+            L = fmaf(__hip_atomic_load(src + q * XPART + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), e, L);
+            O = fmaf(__hip_atomic_load(src + q * XPART + 4 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), e, O);
+        }
+        out[(int64_t)(r0 + k) * D + h * HD + lane] = (h16)(O / L);
     }
-    const int r = pr / H, h = pr % H;
-    out[(int64_t)r * H * HD + h * HD + lane] = (h16)(O / L);
 }
 
 // grid B, 1024 threads: x[b] += bias + Σ split-K partials (residual stream, fp32),
@@ -603,15 +607,11 @@ __device__ SelPart combine_parts(const SelPart* __restrict__ parts) {
 
 // grid B, 64 threads: combine the slices in fixed order, apply the timestamp-mass
 // rule, pick the token, update the window state.
-__global__ __launch_bounds__(64) void select_final_kernel(const float* __restrict__ logits, SelParams P,
-                                                          const int* __restrict__ pos_ptr,
-                                                          const int* __restrict__ prompt,  // [B][P] (-1 = detect)
-                                                          const SelPart* __restrict__ parts,
-                                                          SelState* __restrict__ st, int* __restrict__ cur_tok,
-                                                          int* __restrict__ tokens, int max_tokens) {
+__device__ __forceinline__ void select_final_row(const float* __restrict__ logits, const SelParams& P, int step,
+                                                 const int* __restrict__ prompt, const SelPart* __restrict__ parts,
+                                                 SelState* __restrict__ st, int* __restrict__ cur_tok,
+                                                 int* __restrict__ tokens, int max_tokens) {
     const int b = blockIdx.x;
-    if (threadIdx.x != 0) return;
-    const int step = *pos_ptr;
     SelState s = st[b];
     const int mode = sel_mode(P, step, s);
     if (mode == SEL_PROMPT) {
@@ -659,6 +659,27 @@ __global__ __launch_bounds__(64) void select_final_kernel(const float* __restric
     }
     st[b] = s;
     cur_tok[b] = next;
+}
+
+// grid rows, 64 threads (thread 0 works): the greedy choice for each row.  With
+// `bump` (greedy steps) the last row to finish advances the device step counter, so
+// no separate launch is needed; every row read the counter before it arrived.
+__global__ __launch_bounds__(64) void select_final_kernel(const float* __restrict__ logits, SelParams P,
+                                                          int* __restrict__ pos_ptr,
+                                                          const int* __restrict__ prompt,  // [B][P] (-1 = detect)
+                                                          const SelPart* __restrict__ parts,
+                                                          SelState* __restrict__ st, int* __restrict__ cur_tok,
+                                                          int* __restrict__ tokens, int max_tokens,
+                                                          int* __restrict__ arrive, int bump) {
+    if (threadIdx.x != 0) return;
+    const int step = *pos_ptr;
+    select_final_row(logits, P, step, prompt, parts, st, cur_tok, tokens, max_tokens);
+    if (!bump) return;
+    if (__hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
+        __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(pos_ptr, step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+
 }
 
 // ---------------------------------------------------------------------------
@@ -937,7 +958,7 @@ void launch_dec_self_attn(const float* part, int ks, const float* bias, h16* kc,
 }
 
 void launch_dec_cross_attn(const float* part, int ks, const float* bias, const h16* xk, const h16* xv, int B, int H,
-                           int T, int beam, h16* out, float* ws, hipStream_t s) {
+                           int T, int beam, h16* out, float* ws, int* ticket, hipStream_t s) {
     static const bool legacy = std::getenv("OSW_XATTN_LEGACY") != nullptr;  // A/B switch: one workgroup per (row, head)
     if (legacy || !ws) {
         dec_cross_attn_kernel<<<H * B, 256, 0, s>>>(part, ks, bias, xk, xv, H, B, T, beam, out);
@@ -946,14 +967,13 @@ void launch_dec_cross_attn(const float* part, int ks, const float* bias, const h
     const int W = B / beam;
     const unsigned grid = (unsigned)(((W * H + 7) / 8) * 8 * XCH);
     switch (beam) {
-        case 1: dec_xattn_chunk_kernel<1><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws); break;
-        case 2: dec_xattn_chunk_kernel<2><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws); break;
+        case 1: dec_xattn_chunk_kernel<1><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out); break;
+        case 2: dec_xattn_chunk_kernel<2><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out); break;
         case 3:
-        case 4: dec_xattn_chunk_kernel<4><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws); break;
-        case 5: dec_xattn_chunk_kernel<5><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws); break;
-        default: dec_xattn_chunk_kernel<8><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws); break;
+        case 4: dec_xattn_chunk_kernel<4><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out); break;
+        case 5: dec_xattn_chunk_kernel<5><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out); break;
+        default: dec_xattn_chunk_kernel<8><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out); break;
     }
-    dec_xattn_merge_kernel<<<(unsigned)((B * H + 3) / 4), 256, 0, s>>>(ws, B, H, out);
 }
 
 void launch_dec_resid_ln(const float* part, int ks, int B, int D, const float* bias, float* x, const float* g,
@@ -968,12 +988,12 @@ void launch_dec_reduce_gelu(const float* part, int ks, int B, int N, const float
                                                                                                  bias, y);
 }
 
-void launch_select(const float* logits, int rows, const int* pos, const SelParams& P, const int* prompt,
+void launch_select(const float* logits, int rows, int* pos, const SelParams& P, const int* prompt,
                    const unsigned* supmask, SelState* st, int* cur_tok, int* tokens, int max_tokens, void* sel_parts,
-                   hipStream_t s) {
+                   int* arrive, bool bump, hipStream_t s) {
     select_partial_kernel<<<dim3(rows, SEL_SPLIT), 256, 0, s>>>(logits, P, pos, supmask, st, (SelPart*)sel_parts);
     select_final_kernel<<<rows, 64, 0, s>>>(logits, P, pos, prompt, (const SelPart*)sel_parts, st, cur_tok, tokens,
-                                             max_tokens);
+                                             max_tokens, arrive, bump ? 1 : 0);
 }
 
 void launch_beam(const float* logits, int windows, const int* pos, const SelParams& P, const unsigned* supmask,

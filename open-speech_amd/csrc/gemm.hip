@@ -754,16 +754,6 @@ void launch_gemm_tiled_partial(const GemmArgs& g0, float* part, int ks, hipStrea
     gemm_kernel<EPI_F32><<<grid, NTHR, 0, s>>>(g);
 }
 
-// one workgroup per 64 columns streams the whole K (no partial slabs) and applies the
-// epilogue itself: for the decoder's fc1 (bias + GELU -> fp16) at <= 64 rows
-void launch_gemm_skinny_direct(const GemmArgs& g, hipStream_t s) {
-    switch (g.epi) {
-        case EPI_F16: skinny_mt<EPI_F16>(g, 1, nullptr, s); break;
-        case EPI_F16_GELU: skinny_mt<EPI_F16_GELU>(g, 1, nullptr, s); break;
-        default: break;
-    }
-}
-
 void launch_gemm_skinny(const GemmArgs& g, float* part, hipStream_t s) {
     const int ks = skinny_ksplit(g.N, g.K);
     switch (g.epi) {

@@ -36,7 +36,7 @@ void launch_dec_embed(const h16*, const float*, const int*, const int*, int, int
 void launch_dec_self_attn(const float*, int, const float*, h16*, h16*, const int*, int, int, int, h16*, const int*,
                           hipStream_t);
 void launch_dec_cross_attn(const float*, int, const float*, const h16*, const h16*, int, int, int, int, h16*, float*,
-                           hipStream_t);
+                           int*, hipStream_t);
 void launch_dec_resid_ln(const float*, int, int, int, const float*, float*, const float*, const float*, h16*,
                          const h16*, const float*, const int*, const int*, int, hipStream_t);
 void launch_dec_reduce_gelu(const float*, int, int, int, const float*, h16*, hipStream_t);
@@ -161,12 +161,15 @@ struct osw_ctx {
     int* done_host = nullptr;  // pinned
     float* part = nullptr;     // split-K partial slabs of the decoder GEMMs
     float* xws = nullptr;      // cross-attention per-chunk partials [R][H][XCHUNKS][XPART]
+    int* xticket = nullptr;    // cross-attention arrival tickets [B][H] (zero between launches)
+    int* sel_arrive = nullptr; // select_final arrival counter (zero between launches)
     int64_t part_floats = 0;
 
     // decode-step graph (CH steps per replay), re-captured when its key changes
     hipGraphExec_t dgraph = nullptr;
     std::vector<int64_t> dgraph_key;
     bool capturing = false;
+    bool prof_eager = false;  // profiling mode 2: decode steps launched eagerly so the per-kernel timers see them
     bool use_graph = true;
 
     // profiling
@@ -425,6 +428,10 @@ void setup_workspace(osw_ctx* c) {
     c->bwin = dalloc<BeamWin>(B, o);
     c->bcand = dalloc<char>((size_t)R * beam_cand_bytes(MAX_BEAM), o);
     c->xws = dalloc<float>(R * d.n_text_head * XCHUNKS * XPART, o);
+    c->xticket = dalloc<int>(B * d.n_text_head, o);
+    HIPCHK(hipMemset(c->xticket, 0, (size_t)B * d.n_text_head * sizeof(int)));
+    c->sel_arrive = dalloc<int>(1, o);
+    HIPCHK(hipMemset(c->sel_arrive, 0, sizeof(int)));
     {
         const int64_t Bm = std::min<int64_t>(R, 64);
         const int64_t shapes[][2] = {{3 * Dd, Dd}, {Dd, Dd}, {4 * Dd, Dd}, {Dd, 4 * Dd}, {d.n_vocab, Dd}};
@@ -581,20 +588,15 @@ void decoder_step(osw_ctx* c, int nb, int beam) {
             Timed t(c, CL_XATTN, 2.0 * nb * H * (double)T_ENC * 64 * 2);
             launch_dec_cross_attn(c->part, ks, WF(c, p + ".xq.b"), c->XKV + (2 * l) * xkv_which,
                                   c->XKV + (2 * l + 1) * xkv_which, nb, H, T_ENC, beam, c->dattn, c->xws,
-                                  c->stream);
+                                  c->xticket, c->stream);
         }
         ks = partial(c->dattn, D, WH(c, p + ".xo.w"), D, D);
         launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".xo.b"), c->xd, WF(c, p + ".ln3.g"), WF(c, p + ".ln3.b"),
                             c->xdn, nullptr, nullptr, nullptr, nullptr, ctx, c->stream);
-        static const int fc1_direct = std::getenv("OSW_FC1_SPLIT") ? 0 : 1;  // A/B switch
-        if (fc1_direct && nb <= 64 && D % 128 == 0) {
-            // whole-K workgroups with the bias + GELU epilogue: no slabs, no reduce kernel
-            launch_gemm_skinny_direct(gemm_plain(c->xdn, D, WH(c, p + ".fc1.w"), WF(c, p + ".fc1.b"), nb, 4 * D, D,
-                                                 c->dh, 4 * D, EPI_F16_GELU), c->stream);
-        } else {
-            ks = partial(c->xdn, D, WH(c, p + ".fc1.w"), 4 * D, D);
-            launch_dec_reduce_gelu(c->part, ks, nb, 4 * D, WF(c, p + ".fc1.b"), c->dh, c->stream);
-        }
+        // (a whole-K fc1 with the GELU epilogue fused has only N/64 = 80 workgroups at
+        // turbo: 22.7 us vs 9.6 + 4.7 us for split-K + reduce, measured)
+        ks = partial(c->xdn, D, WH(c, p + ".fc1.w"), 4 * D, D);
+        launch_dec_reduce_gelu(c->part, ks, nb, 4 * D, WF(c, p + ".fc1.b"), c->dh, c->stream);
         ks = partial(c->dh, 4 * D, WH(c, p + ".fc2.w"), D, 4 * D);
         const std::string nx = l + 1 < L ? "dec.l" + std::to_string(l + 1) + ".ln1" : std::string("dec.lnpost");
         launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".fc2.b"), c->xd, WF(c, nx + ".g"), WF(c, nx + ".b"), c->xdn,
@@ -665,18 +667,18 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
     SP.length_penalty = o->length_penalty;
     auto select = [&] {
         launch_select(c->logits, rows, c->pos, SP, c->prompt, c->supmask, c->sel, c->cur_tok, c->tokens, max_tok,
-                      c->selp, c->stream);
+                      c->selp, c->sel_arrive, beam == 1, c->stream);
         if (beam > 1)
             launch_beam(c->logits, nb, c->pos, SP, c->supmask, c->sel, c->selp, c->bcand, c->tokens, c->anc,
                         d.n_text_ctx, c->bwin, c->btok, c->cur_tok, max_tok, c->stream);
     };
     auto one_step = [&] {
         decoder_step(c, rows, beam);
-        select();
-        launch_bump(c->pos, c->stream);
+        select();  // greedy: select_final advances the step counter itself
+        if (beam > 1) launch_bump(c->pos, c->stream);
     };
     const int CH = 8;
-    const bool graph = c->use_graph && !r->logits_dump;
+    const bool graph = c->use_graph && !r->logits_dump && !c->prof_eager;
     if (graph) {
         int32_t lp_bits;
         std::memcpy(&lp_bits, &SP.length_penalty, 4);
@@ -728,7 +730,7 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
                                               c->logits + (size_t)b * V, (size_t)V * 4, hipMemcpyDeviceToHost,
                                               c->stream));
                     select();
-                    launch_bump(c->pos, c->stream);
+                    if (beam > 1) launch_bump(c->pos, c->stream);
                 } else {
                     one_step();
                 }
@@ -1152,7 +1154,9 @@ int osw_set_profiling(osw_ctx* c, int32_t enable) {
     return guard([&] {
         REQUIRE(c, "null ctx");
         std::lock_guard<std::mutex> lk(c->mu);
+        REQUIRE(enable >= 0 && enable <= 2, "profiling mode must be 0, 1 or 2");
         c->prof = enable != 0;
+        c->prof_eager = enable == 2;
         c->pf = osw_profile{};
     });
 }

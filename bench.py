@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--latency-repeats", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-decode-steps", type=int, default=8)
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc_encoder.json"),
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc.json"),
                     help="per-kernel HBM bytes from a rocprofv3 --pmc pass (tools/pmc_summary.py)")
     return ap.parse_args()
 

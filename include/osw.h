@@ -80,6 +80,14 @@ typedef struct osw_decode_opts {
     float patience;              /* <= 0 -> 1; stop once round(beam*patience) hypotheses finished */
     float length_penalty;        /* score / len**length_penalty ranks finished hypotheses */
     int32_t num_hypotheses;      /* <= 0 -> 1 */
+    /* sampling = faster-whisper's temperature > 0 branch (beam 1, num_hypotheses = best_of,
+     * sampling_topk 0): best_of decoder rows per window each draw every token from
+     * softmax(logits / temperature) after the logits rules; the row with the best
+     * sum_logprob / n_tokens**length_penalty is returned.  temperature <= 0: greedy or beam
+     * search as above.  Replaces generate_with_fallback's sampling kwargs [upstream]. */
+    float temperature;
+    int32_t best_of;             /* <= 0 -> 1; windows * best_of <= 5 * max_batch */
+    uint64_t seed;               /* draw seed (counter-hash Gumbel-max, reproducible) */
 } osw_decode_opts;
 
 /* Caller-allocated outputs for n windows. */

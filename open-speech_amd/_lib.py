@@ -34,7 +34,8 @@ class osw_decode_opts(C.Structure):
                 ("prefix_tokens", C.POINTER(C.c_int32)), ("n_prefix", C.c_int32),
                 ("language_tokens", C.POINTER(C.c_int32)),
                 ("beam_size", C.c_int32), ("patience", C.c_float), ("length_penalty", C.c_float),
-                ("num_hypotheses", C.c_int32)]
+                ("num_hypotheses", C.c_int32), ("temperature", C.c_float), ("best_of", C.c_int32),
+                ("seed", C.c_uint64)]
 
 
 class osw_window_result(C.Structure):

@@ -221,7 +221,8 @@ class HipWhisperBackend:
         pcm = decode_audio_bytes(audio)
         opts = TranscribeOptions(task=task, language=language if (language and task == "transcribe") else None,
                                  initial_prompt=prompt or None, temperature=float(temperature or 0.0),
-                                 beam_size=int(os.environ.get("STT_HIP_BEAM_SIZE", "5")))
+                                 beam_size=int(os.environ.get("STT_HIP_BEAM_SIZE", "5")),
+                                 best_of=int(os.environ.get("STT_HIP_BEST_OF", "5")))
         res = m.runner.transcribe(pcm, opts)
         return shape_response(task, res, response_format)
 

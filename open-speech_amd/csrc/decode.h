@@ -21,6 +21,8 @@ struct SelParams {
     int beam;              // hypotheses per window (1 = greedy)
     int num_hyp, max_cand; // beam stop rule: num_hypotheses, round(beam * patience)
     float length_penalty;
+    float inv_temp;        // sampling (temperature > 0): 1 / temperature, else 0
+    unsigned long long seed;
 };
 
 // Per window in beam mode: finished-hypothesis bookkeeping (the best one's tokens

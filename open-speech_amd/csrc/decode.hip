@@ -529,6 +529,21 @@ __device__ __forceinline__ bool tok_masked(const SelParams& P, const RowRules& R
     return masked;
 }
 
+// Gumbel noise for sampling at temperature T: argmax_v(x_v / T + G(seed, row, step, v))
+// is a draw from softmax(x / T) over the kept tokens (Gumbel-max).  G = -log(-log u),
+// u from a splitmix64 hash of (seed, row, step, token) on 23 bits, so a draw does not
+// depend on slice or lane order (oracle/decode.py restates it bit for bit).
+__device__ __forceinline__ float gumbel_noise(unsigned long long seed, int row, int step, int v) {
+    unsigned long long z = seed + 0x9E3779B97F4A7C15ull * (unsigned long long)(row + 1) +
+                           0xD1B54A32D192ED03ull * (unsigned long long)(step + 1) +
+                           0x94D049BB133111EBull * (unsigned long long)(v + 1);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    const float u = ((float)(unsigned)(z >> 41) + 0.5f) * (1.0f / 8388608.0f);
+    return -logf(-logf(u));
+}
+
 // grid (B, SEL_SPLIT), 256 threads
 __global__ __launch_bounds__(256) void select_partial_kernel(const float* __restrict__ logits, SelParams P,
                                                              const int* __restrict__ pos_ptr,
@@ -555,10 +570,13 @@ __global__ __launch_bounds__(256) void select_partial_kernel(const float* __rest
         }
         if (tok_masked(P, R, supmask, v)) continue;
         lse_add(m_all, s_all, xv);
-        a_all = amax(a_all, ArgMax{xv, v});
+        // sampling: a_all / a_ts pick the Gumbel-perturbed maximum; a_text stays the plain
+        // maximum (the timestamp-mass rule compares against it)
+        const float key = P.inv_temp > 0.f ? xv * P.inv_temp + gumbel_noise(P.seed, b, step, v) : xv;
+        a_all = amax(a_all, ArgMax{key, v});
         if (v >= P.tb) {
             lse_add(m_ts, s_ts, xv);
-            a_ts = amax(a_ts, ArgMax{xv, v});
+            a_ts = amax(a_ts, ArgMax{key, v});
         } else {
             a_text = amax(a_text, ArgMax{xv, v});
         }
@@ -638,14 +656,18 @@ __device__ __forceinline__ void select_final_row(const float* __restrict__ logit
     }
     const int n = s.n_sampled;
     int next = r.i_all;
-    float lp = r.v_all - lse_all;
+    float lse = lse_all;
     if (P.with_ts) {
         const float lse_ts = r.m_ts == -INFINITY ? -INFINITY : r.m_ts + __logf(r.s_ts);
         if (lse_ts - lse_all > r.v_text - lse_all) {  // timestamp mass wins: text suppressed
             next = r.i_ts;
-            lp = r.v_ts - lse_ts;
+            lse = lse_ts;
         }
     }
+    // log-prob of the pick under the rule-masked, untempered distribution (what openai /
+    // faster-whisper accumulate); sampling keys are perturbed, so read the logit back
+    const float lp =
+        (P.inv_temp > 0.f ? logits[(int64_t)b * P.V + next] : (next == r.i_all ? r.v_all : r.v_ts)) - lse;
     s.sum_lp += lp;
     if (next == P.eot) {
         s.done = 1;

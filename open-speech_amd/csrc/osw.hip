@@ -552,11 +552,13 @@ void encode(osw_ctx* c, const osw_window* wins, int n) {
 // One decoder step for nb windows.  Every projection is a split-K skinny GEMM whose
 // partial slabs are reduced by the kernel that consumes them (self/cross attention
 // for q/k/v, residual+LayerNorm for the out-projections and fc2, GELU for fc1).
-// nb = decoder rows (windows x beam); rows of one window are adjacent.
-void decoder_step(osw_ctx* c, int nb, int beam) {
+// nb = decoder rows (windows x group); the `group` rows of one window are adjacent
+// (beam hypotheses or best_of samples); `gather` = beam rows read the self-K/V cache
+// through the ancestry table.
+void decoder_step(osw_ctx* c, int nb, int group, bool gather) {
     const osw_dims& d = c->d;
     const int D = d.n_text_state, H = d.n_text_head, L = d.n_text_layer, ctx = d.n_text_ctx;
-    const int64_t xkv_which = (int64_t)(nb / beam) * H * T_ENC * 64;
+    const int64_t xkv_which = (int64_t)(nb / group) * H * T_ENC * 64;
     const int64_t kv_layer = (int64_t)nb * H * ctx * 64;
     REQUIRE(nb <= c->R && D <= 1280, "decoder step: rows <= capacity and D <= 1280");
     // <= 64 rows: split-K skinny GEMM; more (beam search): one slab from the tiled GEMM
@@ -579,7 +581,7 @@ void decoder_step(osw_ctx* c, int nb, int beam) {
         const std::string p = "dec.l" + std::to_string(l);
         int ks = partial(c->xdn, D, WH(c, p + ".qkv.w"), 3 * D, D);
         launch_dec_self_attn(c->part, ks, WF(c, p + ".qkv.b"), c->kc + l * kv_layer, c->vc + l * kv_layer, c->pos, nb,
-                             H, ctx, c->dattn, beam > 1 ? c->anc : nullptr, c->stream);
+                             H, ctx, c->dattn, gather ? c->anc : nullptr, c->stream);
         ks = partial(c->dattn, D, WH(c, p + ".o.w"), D, D);
         launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".o.b"), c->xd, WF(c, p + ".ln2.g"), WF(c, p + ".ln2.b"),
                             c->xdn, nullptr, nullptr, nullptr, nullptr, ctx, c->stream);
@@ -587,7 +589,7 @@ void decoder_step(osw_ctx* c, int nb, int beam) {
         {
             Timed t(c, CL_XATTN, 2.0 * nb * H * (double)T_ENC * 64 * 2);
             launch_dec_cross_attn(c->part, ks, WF(c, p + ".xq.b"), c->XKV + (2 * l) * xkv_which,
-                                  c->XKV + (2 * l + 1) * xkv_which, nb, H, T_ENC, beam, c->dattn, c->xws,
+                                  c->XKV + (2 * l + 1) * xkv_which, nb, H, T_ENC, group, c->dattn, c->xws,
                                   c->xticket, c->stream);
         }
         ks = partial(c->dattn, D, WH(c, p + ".xo.w"), D, D);
@@ -613,11 +615,15 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
     const int V = d.n_vocab;
     const int n_pre = o->n_prefix;
     REQUIRE(n_pre >= 0 && (n_pre == 0 || o->prefix_tokens), "bad prefix");
-    const int beam = std::max(1, o->beam_size);
-    REQUIRE(beam <= MAX_BEAM, "beam_size > 8");
-    const int rows = nb * beam;
-    REQUIRE(rows <= c->R, "windows x beam_size exceeds the decoder row capacity (5 x max_batch)");
-    REQUIRE(beam == 1 || !r->logits_dump, "logits dump is greedy-only");
+    // temperature > 0 (faster-whisper's sampling branch): beam 1 and best_of independent
+    // sampled rows per window, the best one kept; otherwise beam search or greedy
+    const bool sampling = o->temperature > 0.f;
+    const int beam = sampling ? 1 : std::max(1, o->beam_size);
+    const int group = sampling ? std::max(1, o->best_of) : beam;  // decoder rows per window
+    REQUIRE(group <= MAX_BEAM, "beam_size / best_of > 8");
+    const int rows = nb * group;
+    REQUIRE(rows <= c->R, "windows x beam_size (best_of) exceeds the decoder row capacity (5 x max_batch)");
+    REQUIRE(group == 1 || !r->logits_dump, "logits dump needs one decoder row per window");
     REQUIRE(V <= SEL_SPLIT * 4096, "vocabulary too large for the selection kernels");
     const int P = n_pre + 3 + (o->without_timestamps ? 1 : 0);
     const int max_len = std::min(o->max_length > 0 ? o->max_length : d.n_text_ctx, d.n_text_ctx);
@@ -625,8 +631,8 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
     // one prompt per decoder row (the beam rows of a window share it)
     std::vector<int> prompt((size_t)rows * P);
     for (int b = 0; b < nb; ++b)
-        for (int k = 0; k < beam; ++k) {
-            int* pr = &prompt[((size_t)b * beam + k) * P];
+        for (int k = 0; k < group; ++k) {
+            int* pr = &prompt[((size_t)b * group + k) * P];
             for (int i = 0; i < n_pre; ++i) pr[i] = o->prefix_tokens[(size_t)b * n_pre + i];
             pr[n_pre] = o->sot;
             pr[n_pre + 1] = o->language_tokens ? o->language_tokens[b] : o->language_token;  // -1: detect
@@ -665,6 +671,8 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
     SP.num_hyp = std::max(1, o->num_hypotheses);
     SP.max_cand = std::max(1, (int)std::lround(beam * (o->patience > 0.f ? o->patience : 1.f)));
     SP.length_penalty = o->length_penalty;
+    SP.inv_temp = sampling ? 1.f / o->temperature : 0.f;
+    SP.seed = o->seed;
     auto select = [&] {
         launch_select(c->logits, rows, c->pos, SP, c->prompt, c->supmask, c->sel, c->cur_tok, c->tokens, max_tok,
                       c->selp, c->sel_arrive, beam == 1, c->stream);
@@ -673,19 +681,20 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
                         d.n_text_ctx, c->bwin, c->btok, c->cur_tok, max_tok, c->stream);
     };
     auto one_step = [&] {
-        decoder_step(c, rows, beam);
+        decoder_step(c, rows, group, beam > 1);
         select();  // greedy: select_final advances the step counter itself
         if (beam > 1) launch_bump(c->pos, c->stream);
     };
     const int CH = 8;
     const bool graph = c->use_graph && !r->logits_dump && !c->prof_eager;
     if (graph) {
-        int32_t lp_bits;
+        int32_t lp_bits, it_bits;
         std::memcpy(&lp_bits, &SP.length_penalty, 4);
+        std::memcpy(&it_bits, &SP.inv_temp, 4);
         std::vector<int64_t> key = {nb, P, n_pre, max_len, o->eot, o->no_speech, o->no_timestamps,
                                     o->timestamp_begin, o->blank, o->first_lang, o->n_langs, o->suppress_blank,
                                     o->without_timestamps, o->max_initial_timestamp_index, beam, SP.num_hyp,
-                                    SP.max_cand, lp_bits};
+                                    SP.max_cand, lp_bits, group, it_bits, (int64_t)SP.seed};
         if (!c->dgraph || key != c->dgraph_key) {
             if (c->dgraph) {
                 HIPCHK(hipGraphExecDestroy(c->dgraph));
@@ -724,7 +733,7 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
             } else {
                 const int samp = steps - (P - 1);
                 if (r->logits_dump && samp >= 0 && samp < r->dump_steps) {
-                    decoder_step(c, rows, beam);
+                    decoder_step(c, rows, group, beam > 1);
                     for (int b = 0; b < nb; ++b)
                         HIPCHK(hipMemcpyAsync(r->logits_dump + ((size_t)b * r->dump_steps + samp) * V,
                                               c->logits + (size_t)b * V, (size_t)V * 4, hipMemcpyDeviceToHost,
@@ -752,7 +761,7 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
     // read back
     std::vector<SelState> st(rows);
     HIPCHK(hipMemcpyAsync(st.data(), c->sel, rows * sizeof(SelState), hipMemcpyDeviceToHost, c->stream));
-    std::vector<int> toks((size_t)nb * max_tok);
+    std::vector<int> toks((size_t)(beam > 1 ? nb : rows) * max_tok);
     std::vector<BeamWin> bw(nb);
     if (beam > 1) {
         HIPCHK(hipMemcpyAsync(toks.data(), c->btok, toks.size() * 4, hipMemcpyDeviceToHost, c->stream));
@@ -761,12 +770,22 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
         HIPCHK(hipMemcpyAsync(toks.data(), c->tokens, toks.size() * 4, hipMemcpyDeviceToHost, c->stream));
     }
     HIPCHK(hipStreamSynchronize(c->stream));
+    // best_of: the sample with the highest sum_logprob / n**length_penalty (first on ties)
+    auto norm = [&](const SelState& q) {
+        if (q.n_sampled == 0) return o->length_penalty != 0.f ? -INFINITY : q.sum_lp;
+        return q.sum_lp / std::pow((float)q.n_sampled, o->length_penalty);
+    };
     for (int b = 0; b < nb; ++b) {
-        const SelState& sp = st[(size_t)b * beam];
+        size_t best = (size_t)b * group;
+        if (sampling)
+            for (int k = 1; k < group; ++k)
+                if (norm(st[(size_t)b * group + k]) > norm(st[best])) best = (size_t)b * group + k;
+        const SelState& sp = st[best];
         const int n0 = beam > 1 ? bw[b].best_len : sp.n_sampled;
         const int n = std::min(n0, std::min(max_tok, r->max_tokens));
         r->n_tokens[b] = n;
-        for (int i = 0; i < n; ++i) r->tokens[(size_t)b * r->max_tokens + i] = toks[(size_t)b * max_tok + i];
+        const int* src = &toks[(beam > 1 ? (size_t)b : best) * max_tok];
+        for (int i = 0; i < n; ++i) r->tokens[(size_t)b * r->max_tokens + i] = src[i];
         r->sum_logprob[b] = beam > 1 ? bw[b].best_raw : sp.sum_lp;
         r->no_speech_prob[b] = sp.nsp;
         r->language[b] = sp.lang;

@@ -8,8 +8,10 @@ encoded and decoded together on the GPU (grouped by prompt length, since every
 window of one decode call shares its prompt length).
 
 Semantics restated (beam search width ``beam_size`` — 5 in the reference, 1 = greedy
-for the parity mode — and a single temperature 0.0: the reference passes a scalar
-``temperature`` at ``src/backends/faster_whisper.py:238``, so there is no fallback):
+for the parity mode — at temperature 0.0; the reference passes a scalar ``temperature``
+at ``src/backends/faster_whisper.py:238``, so there is no fallback, and a request with
+temperature > 0 takes faster-whisper's sampling branch: ``best_of`` samples per window,
+the best kept, and the previous-text prompt reset when temperature > 0.5):
   content_frames = n_frames - 1; segment_size = min(3000, content_frames - seek)
   prompt = [<|startofprev|>] + previous_tokens[-223:] (if any) + [sot, lang, task]
   avg_logprob = sum_logprob / (len(tokens) + 1); compression_ratio of the window text
@@ -47,11 +49,14 @@ class TranscribeOptions:
     beam_size: int = 5             # faster-whisper / reference default (src/backends/faster_whisper.py:237)
     patience: float = 1.0
     length_penalty: float = 1.0
+    best_of: int = 5               # faster-whisper default; used when temperature > 0
+    prompt_reset_on_temperature: float = 0.5
+    seed: int = 0
 
     def key(self):
         return (self.task, self.language, self.initial_prompt, self.condition_on_previous_text,
                 self.without_timestamps, tuple(self.suppress_tokens), self.suppress_blank, self.beam_size,
-                self.patience, self.length_penalty)
+                self.patience, self.length_penalty, self.temperature, self.best_of)
 
 
 @dataclass
@@ -134,8 +139,11 @@ def transcribe_clips(engine, pcm_list: list, opts: TranscribeOptions, tok: Whisp
         s.done = s.content_frames <= 0
         states.append(s)
     max_init = int(round(opts.max_initial_timestamp / TIME_PRECISION))
-    beam = max(1, int(opts.beam_size))
-    B = max(1, min(engine.max_batch, getattr(engine, "max_rows", engine.max_batch) // beam))
+    sampling = opts.temperature > 0
+    beam = 1 if sampling else max(1, int(opts.beam_size))
+    group = max(1, int(opts.best_of)) if sampling else beam  # decoder rows per window
+    B = max(1, min(engine.max_batch, getattr(engine, "max_rows", engine.max_batch) // group))
+    calls = 0
     while True:
         active = [s for s in states if not s.done]
         if not active:
@@ -158,7 +166,9 @@ def transcribe_clips(engine, pcm_list: list, opts: TranscribeOptions, tok: Whisp
                 cfg = DecodeConfig(task=opts.task, language_token=None, suppress_tokens=suppress,
                                    suppress_blank=opts.suppress_blank, without_timestamps=opts.without_timestamps,
                                    max_initial_timestamp_index=max_init, beam_size=beam, patience=opts.patience,
-                                   length_penalty=opts.length_penalty)
+                                   length_penalty=opts.length_penalty, temperature=opts.temperature,
+                                   best_of=opts.best_of, seed=(opts.seed + 0x9E3779B1 * calls) & (2**64 - 1))
+                calls += 1
                 prefixes = [p for _, p in chunk] if _plen else None
                 outs = engine.decode(len(chunk), cfg, prefix=prefixes, languages=langs)
                 for (s, _), w, out in zip(chunk, wins, outs):
@@ -199,7 +209,7 @@ def _consume(s: _ClipState, win, out, opts: TranscribeOptions, tok: WhisperToken
                                          text=txt, tokens=list(t), temperature=opts.temperature,
                                          avg_logprob=avg_logprob, compression_ratio=cr,
                                          no_speech_prob=out.no_speech_prob))
-    if not opts.condition_on_previous_text:
+    if not opts.condition_on_previous_text or opts.temperature > opts.prompt_reset_on_temperature:
         s.prompt_reset_since = len(s.all_tokens)
     s.seek = new_seek
     s.done = s.seek >= s.content_frames

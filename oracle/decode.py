@@ -250,3 +250,37 @@ def beam_from_encoder(oracle, xkv, st, *, language=None, task=None, prev_tokens=
         if f[0] > best[0]:
             best = f
     return WindowResult(tokens=best[2], sum_logprob=best[1], no_speech_prob=nsp, language=lang)
+
+
+# ---------------------------------------------------------------------------
+# Sampling at temperature > 0 — faster-whisper's sampling branch of
+# ``generate_with_fallback`` [upstream] (``beam_size=1, num_hypotheses=best_of,
+# sampling_topk=0, sampling_temperature=T``).  The device draws every token by the
+# Gumbel-max trick on a counter hash (``gumbel_noise`` in csrc/decode.hip), so a
+# draw is reproducible from (seed, decoder row, step, token); this restates that
+# draw bit for bit in float32.  PARITY UNPINNED against CTranslate2, whose RNG
+# stream cannot be reproduced; what is pinned is the draw rule: argmax over the
+# rule-masked logits of x / T + G is a sample of softmax(x / T) over those tokens.
+# ---------------------------------------------------------------------------
+_M64 = 0xFFFFFFFFFFFFFFFF
+
+
+def gumbel_noise(seed: int, row: int, step: int, v: np.ndarray) -> np.ndarray:
+    """float32 Gumbel(0, 1) noise for tokens ``v`` (splitmix64 finaliser, 23-bit uniform)."""
+    v = np.asarray(v, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        base = (seed + 0x9E3779B97F4A7C15 * (row + 1) + 0xD1B54A32D192ED03 * (step + 1)) & _M64
+        z = np.uint64(base) + np.uint64(0x94D049BB133111EB) * (v + np.uint64(1))
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    u = ((z >> np.uint64(41)).astype(np.float32) + np.float32(0.5)) * np.float32(1.0 / 8388608.0)
+    return -np.log(-np.log(u))
+
+
+def sample_token(x_processed: np.ndarray, inv_temp: float, seed: int, row: int, step: int) -> int:
+    """One draw from softmax(x / T) over the finite (kept) entries of the processed logits;
+    ties go to the lowest token id."""
+    idx = np.nonzero(np.isfinite(x_processed))[0]
+    key = x_processed[idx].astype(np.float32) * np.float32(inv_temp) + gumbel_noise(seed, row, step, idx)
+    return int(idx[int(np.argmax(key))])

@@ -247,3 +247,48 @@ def test_sibling_shares_weights(tiny_engine):
                 assert x.tokens == y.tokens and x.sum_logprob == y.sum_logprob
     finally:
         sib.close()
+
+
+def test_sampling_draws_match_oracle(tiny_engine):
+    """temperature > 0: every pick is argmax(x / T + Gumbel(seed, row, step, token)) over
+    the rule-masked logits.  Replayed by the oracle on the GPU's own logits: ids exact;
+    the same seed gives the same ids; T -> 0 gives the greedy ids."""
+    from oracle import decode as odec
+    d, eng, w = tiny_engine
+    st = D.SpecialTokens.for_vocab(d.n_vocab)
+    eng.log_mel([synth.chirp_clip(11, 30.0)])
+    eng.encode([(0, 0, 3000)])
+    sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+    T, seed = 1.0, 77
+    cfg = DecodeConfig(suppress_tokens=sup, max_length=64, temperature=T, best_of=1, seed=seed)
+    out = eng.decode(1, cfg, dump_steps=8)[0]
+    opts = odec.DecodeOptions(suppress_tokens=sup, max_length=64)
+    hist = []
+    for i in range(min(8, len(out.tokens) + 1)):
+        x = odec.process_logits(out.logits[i], hist, st, opts)
+        t = odec.sample_token(x, 1.0 / T, seed, 0, 2 + i)   # prompt = sot, lang, task: first pick at step 2
+        assert t == (out.tokens[i] if i < len(out.tokens) else st.eot), i
+        if t == st.eot:
+            break
+        hist.append(t)
+    assert eng.decode(1, cfg)[0].tokens == out.tokens
+    greedy = eng.decode(1, DecodeConfig(suppress_tokens=sup, max_length=64))[0]
+    cold = eng.decode(1, DecodeConfig(suppress_tokens=sup, max_length=64, temperature=1e-5, best_of=1, seed=5))[0]
+    assert cold.tokens == greedy.tokens
+
+
+def test_sampling_best_of_picks_best_row(tiny_engine):
+    """best_of rows per window: the returned sample is the row with the best
+    sum_logprob / n; rows never mix across windows (each window alone == in a batch)."""
+    d, eng, w = tiny_engine
+    sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+    clips = [synth.chirp_clip(21, 30.0), synth.chirp_clip(22, 9.0)]
+    cfg = DecodeConfig(suppress_tokens=sup, max_length=48, temperature=0.9, best_of=3, seed=3)
+    both = eng.transcribe_batch(clips, cfg)
+    assert eng.transcribe_batch(clips, cfg)[0].tokens == both[0].tokens
+    one = DecodeConfig(suppress_tokens=sup, max_length=48, temperature=0.9, best_of=1, seed=3)
+    # row k of window 0 is decoder row k both times: best_of=3 contains best_of=1's sample
+    first = eng.transcribe_batch(clips[:1], one)[0]
+    assert both[0].sum_logprob / max(1, len(both[0].tokens)) >= first.sum_logprob / max(1, len(first.tokens)) - 1e-6
+    for o in both:
+        assert np.isfinite(o.sum_logprob)

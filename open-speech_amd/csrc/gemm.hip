@@ -137,7 +137,9 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
 #pragma unroll
                 for (int ni = 0; ni < 4; ++ni) {
                     const int n = n0 + wn * 64 + ni * 16 + (lane & 15);
-                    if (n < g.N) C[(int64_t)m * g.ldc + n] = acc[mi][ni][i];
+                    if (n < g.N)  // written through L2, like the skinny slabs
+                        __hip_atomic_store(&C[(int64_t)m * g.ldc + n], acc[mi][ni][i], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
         return;
@@ -151,7 +153,14 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni) {
                 const int n = n0 + wn * 64 + ni * 16 + (lane & 15);
-                if (n < g.N) store_one<EPI>(g, m, n, acc[mi][ni][i]);
+                if (n >= g.N) continue;
+                if constexpr (EPI == EPI_F32) {  // decoder logits: written through L2 for the select kernels
+                    const float v = g.bias ? acc[mi][ni][i] + g.bias[n] : acc[mi][ni][i];
+                    const int64_t grp = m / g.c_grp_rows, r = m % g.c_grp_rows;
+                    __hip_atomic_store((float*)g.C + grp * g.c_grp_stride + r * g.ldc + n, v, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                } else
+                    store_one<EPI>(g, m, n, acc[mi][ni][i]);
             }
         }
 }
@@ -662,7 +671,10 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
             const int m = mt * 16 + gq * 4 + i;
             if (m >= g.M) continue;
             if constexpr (DIRECT) store_one<EPI>(g, m, col, acc[mt][i]);
-            else part[((int64_t)ks * g.M + m) * g.N + col] = acc[mt][i];
+            // slabs are written through L2 (device-scope stores): no dirty lines left for
+            // the kernel-boundary write-back to drain before the consumer can start
+            else __hip_atomic_store(&part[((int64_t)ks * g.M + m) * g.N + col], acc[mt][i], __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
         }
 }
 

@@ -561,6 +561,7 @@ void decoder_step(osw_ctx* c, int nb, int group, bool gather) {
     const int64_t xkv_which = (int64_t)(nb / group) * H * T_ENC * 64;
     const int64_t kv_layer = (int64_t)nb * H * ctx * 64;
     REQUIRE(nb <= c->R && D <= 1280, "decoder step: rows <= capacity and D <= 1280");
+    REQUIRE(ctx <= 448, "decoder self-attention holds at most 448 positions");
     // <= 64 rows: split-K skinny GEMM; more (beam search): one slab from the tiled GEMM
     auto partial = [&](const h16* A, int lda, const h16* Wt, int N, int K) {
         if (nb > 64) {

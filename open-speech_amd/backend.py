@@ -126,7 +126,7 @@ class HipWhisperBackend:
                     engines.append(eng)
                     # extra lanes on the same GPU share the weights: one batch's encoder
                     # (MFMA-bound) overlaps another's decoder (HBM/latency-bound)
-                    for _ in range(max(1, int(os.environ.get("STT_HIP_LANES", "2"))) - 1):
+                    for _ in range(max(1, int(os.environ.get("STT_HIP_LANES", "3"))) - 1):
                         if hasattr(eng, "sibling"):
                             engines.append(eng.sibling())
             except Exception:

@@ -112,7 +112,12 @@ __global__ __launch_bounds__(256, 2) void enc_attn_kernel(const h16* __restrict_
                 sc[qt][t] = a;
             }
         }
-        // ---- online softmax (lane-local per query; 4 lanes g=0..3 share a query)
+        // ---- online softmax (lane-local per query; 4 lanes g=0..3 share a query).  VALU
+        // is this loop's bound at d = 64 (≈ 2x the MFMA cycles), so: the running max is
+        // kept on raw scores and the 1/sqrt(d)*log2(e) scale folds into one FMA per score,
+        // keys past T are masked only in the last tile, and exp2 is the bare v_exp_f32
+        // (results below 2^-126 flush to 0, irrelevant next to the row maximum's 1).
+        const bool tail = k0 + KB > T;
         h16x8 pf[2][2];
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) {
@@ -121,24 +126,22 @@ __global__ __launch_bounds__(256, 2) void enc_attn_kernel(const h16* __restrict_
             for (int t = 0; t < 4; ++t)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const int key = k0 + 16 * t + 4 * g + i;
-                    float v = sc[qt][t][i] * cs;
-                    v = key < T ? v : -INFINITY;
-                    sc[qt][t][i] = v;
-                    mx = fmaxf(mx, v);
+                    if (tail && k0 + 16 * t + 4 * g + i >= T) sc[qt][t][i] = -INFINITY;
+                    mx = fmaxf(mx, sc[qt][t][i]);
                 }
             mx = fmaxf(mx, xor_lane<16>(mx));
             mx = fmaxf(mx, xor_lane<32>(mx));
             const float mnew = fmaxf(mrun[qt], mx);
-            const float alpha = exp2f(mrun[qt] - mnew);
+            const float alpha = __builtin_amdgcn_exp2f((mrun[qt] - mnew) * cs);
             mrun[qt] = mnew;
+            const float mcs = -mnew * cs;
             float ls = 0.f;
             float p[4][4];
 #pragma unroll
             for (int t = 0; t < 4; ++t)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    p[t][i] = exp2f(sc[qt][t][i] - mnew);
+                    p[t][i] = __builtin_amdgcn_exp2f(fmaf(sc[qt][t][i], cs, mcs));
                     ls += p[t][i];
                 }
             lrun[qt] = lrun[qt] * alpha + ls;

@@ -611,7 +611,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
 #pragma unroll
         for (int u = 0; u < CK; ++u) {
             const int st = min(c * CK + u, nsteps - 1);
-            wf[u] = *(const h16x8*)(wrow + 32 * st);
+            wf[u] = *(const h16x8*)(wrow + 32 * st);  // (nt loads measured 8.1 vs 7.2 us: the weights are re-read every step)
         }
     };
     f32x4 acc[MT];

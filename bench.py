@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--max-length", type=int, default=448)
     ap.add_argument("--latency-repeats", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--beam5", type=int, default=1, help="also time one isolated beam-5 step (the reference default)")
     ap.add_argument("--cpu-decode-steps", type=int, default=8)
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc.json"),
                     help="per-kernel HBM bytes from a rocprofv3 --pmc pass (tools/pmc_summary.py)")
@@ -203,6 +204,17 @@ def main():
         roof["measured"] = "isolated roofline pass after the timed region (1 lane, HIP events on the lane's stream)"
         stages = {k: {"ms": round(v[0], 2), "launches": int(v[2])} for k, v in cands.items()}
 
+        # the reference's own decoding (beam_size=5, src/backends/faster_whisper.py:237): one
+        # isolated 64-clip step on lane 0, reported beside the greedy headline
+        beam5 = None
+        if a.beam5:
+            bcfg = DecodeConfig(suppress_tokens=sup, max_length=a.max_length, beam_size=5)
+            torch.cuda.synchronize(dev)
+            tb = time.perf_counter()
+            eng.transcribe_batch(None, bcfg, device_pcm=allpcm.data_ptr(),
+                                 offsets=np.arange(B + 1, dtype=np.int64) * allpcm.shape[-1])
+            beam5 = round(B * 30.0 / (time.perf_counter() - tb), 2)
+
         # p50 latency at batch 1 (BASELINE configs[1])
         lat = []
         one = torch.from_numpy(make_clips(1, offset=999)).to(dev)
@@ -228,6 +240,7 @@ def main():
                        "lanes_per_gpu": len(dp.lanes)},
             "tokens_per_clip": round(tokens_per_clip, 1),
             "p50_latency_ms_b1": None if p50 is None else round(p50, 2),
+            "beam5_audio_sec_per_sec_1lane": beam5,
             "realtime_factor": round(value, 1),
             "roofline": roof,
             "rooflines": {k: {kk: v[kk] for kk in ("achieved", "unit", "frac", "avg_launch_ms")} for k, v in roofs.items()},

@@ -229,7 +229,7 @@ constexpr int XCH = XCHUNKS, XKEYS = 192, XU = XKEYS / 32;
 static_assert(XCH == 8, "the (window, head) -> XCD map assumes 8 chunks");
 
 template <int NB>
-__global__ __launch_bounds__(256) void dec_xattn_chunk_kernel(const float* __restrict__ part, int ks,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 : NB > 1 ? 5 : 1))) void dec_xattn_chunk_kernel(const float* __restrict__ part, int ks,
                                                               const float* __restrict__ bias,
                                                               const h16* __restrict__ xk, const h16* __restrict__ xv,
                                                               int H, int W, int T, int beam, float* __restrict__ ws,
@@ -513,8 +513,9 @@ __device__ __forceinline__ RowRules row_rules(const SelParams& P, const SelState
     if (P.with_ts && s.last_ts > 0) R.ts_block = (R.last_ts && !R.pen_ts) ? s.last_ts : s.last_ts + 1;
     return R;
 }
-__device__ __forceinline__ bool tok_masked(const SelParams& P, const RowRules& R, const unsigned* supmask, int v) {
-    bool masked = (supmask[v >> 5] >> (v & 31)) & 1u;
+// word = supmask[v >> 5], the suppress-token bitmap word holding token v
+__device__ __forceinline__ bool tok_masked_w(const SelParams& P, const RowRules& R, unsigned word, int v) {
+    bool masked = (word >> (v & 31)) & 1u;
     if (P.suppress_blank && R.n == 0 && (v == P.blank || v == P.eot)) masked = true;
     if (P.with_ts) {
         if (v == P.no_ts) masked = true;
@@ -529,6 +530,9 @@ __device__ __forceinline__ bool tok_masked(const SelParams& P, const RowRules& R
         }
     }
     return masked;
+}
+__device__ __forceinline__ bool tok_masked(const SelParams& P, const RowRules& R, const unsigned* supmask, int v) {
+    return tok_masked_w(P, R, supmask[v >> 5], v);
 }
 
 // Gumbel noise for sampling at temperature T: argmax_v(x_v / T + G(seed, row, step, v))
@@ -611,7 +615,7 @@ __global__ __launch_bounds__(256) void select_partial_kernel(const float* __rest
     }
 }
 
-__device__ SelPart combine_parts(const SelPart* __restrict__ parts) {
+__device__ __forceinline__ SelPart combine_parts(const SelPart* __restrict__ parts) {
     SelPart r = parts[0];
     for (int i = 1; i < SEL_SPLIT; ++i) {
         const SelPart& q = parts[i];
@@ -734,25 +738,24 @@ __device__ __forceinline__ ArgMax block_amax(ArgMax a, ArgMax* red) {
     return r;
 }
 
-constexpr int BEAM_SLICES = 4;   // vocabulary slices per row in beam_topk
+constexpr int BEAM_SLICES = 16;  // vocabulary slices per row in beam_topk
+constexpr int TOPK_VPT = 16;     // logits one thread loads per batch in beam_topk
 constexpr int MAXK2 = 2 * MAX_BEAM;
-
-__device__ __forceinline__ bool cand_better(float s, int i, float t, int j) {
-    return s > t || (s == t && i < j);
-}
+static_assert(BEAM_SLICES * 256 * TOPK_VPT >= SEL_SPLIT * 4096, "osw.hip admits V <= SEL_SPLIT * 4096: one batch per slice");
 
 // grid (rows, BEAM_SLICES), 256 threads: the top 2*beam (score desc, flat index asc)
-// of one vocabulary slice of one row.  Each thread keeps a sorted list of its own
-// best 2*beam entries in registers (insertion, visited in index order), then the
-// lists are merged pairwise through LDS in 8 levels.
+// of one vocabulary slice of one row.  Each thread loads its TOPK_VPT logits of the
+// slice in one batch (one memory latency instead of one per logit) and scores them
+// in registers; then the block pops its best entry 2*beam times (wave DPP argmax +
+// one LDS exchange per pop; only the owner of a popped entry rescans its slots).
+// A sorted per-thread insertion list cost ~8x more VALU (it ran 141 us here).
 __global__ __launch_bounds__(256) void beam_topk_kernel(const float* __restrict__ logits, SelParams P,
                                                         const int* __restrict__ pos_ptr,
                                                         const unsigned* __restrict__ supmask,
                                                         const SelState* __restrict__ st,
                                                         const SelPart* __restrict__ parts, BeamCand* __restrict__ cand) {
     __shared__ float stat[3];
-    __shared__ float lv[256][MAXK2 + 1];
-    __shared__ int li[256][MAXK2 + 1];
+    __shared__ ArgMax red[2][4];
     const int row = blockIdx.x, sl = blockIdx.y, tid = threadIdx.x;
     const int step = *pos_ptr;
     const SelState s = st[row];
@@ -771,67 +774,63 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(const float* __restrict_
         stat[1] = lse_ts;
         stat[2] = (P.with_ts && lse_ts - lse_all > r.v_text - lse_all) ? 1.f : 0.f;
     }
+    const int per = (P.V + BEAM_SLICES - 1) / BEAM_SLICES;  // <= 256 * TOPK_VPT (host-checked)
+    const int lo = sl * per, hi = min(P.V, lo + per);
+    const float* x = logits + (int64_t)row * P.V;
+    float xv[TOPK_VPT];
+    unsigned mw[TOPK_VPT];  // suppress-mask words, loaded with the logits
+#pragma unroll
+    for (int u = 0; u < TOPK_VPT; ++u) {  // issued before the barrier: overlaps the prelude
+        const int v = lo + u * 256 + tid;
+        xv[u] = v < hi ? x[v] : 0.f;
+        mw[u] = v < hi ? supmask[v >> 5] : 0u;
+    }
     __syncthreads();
     const float lse_all = stat[0], lse_ts = stat[1];
     const bool ts_wins = stat[2] != 0.f;
     const RowRules R = row_rules(P, s);
-    const int per = (P.V + BEAM_SLICES - 1) / BEAM_SLICES;
-    const int lo = sl * per, hi = min(P.V, lo + per);
-    const float* x = logits + (int64_t)row * P.V;
-    float tv[MAXK2];
-    int ti[MAXK2];
-#pragma unroll
-    for (int j = 0; j < MAXK2; ++j) { tv[j] = -INFINITY; ti[j] = INT_MAX; }
     const int base = k * P.V;
-    for (int v = lo + tid; v < hi; v += 256) {
+    // score the thread's logits in place; `used` marks taken, out-of-slice and NaN slots
+    unsigned used = 0;
+#pragma unroll
+    for (int u = 0; u < TOPK_VPT; ++u) {
+        const int v = lo + u * 256 + tid;
         float lp = -INFINITY;
-        if (!tok_masked(P, R, supmask, v)) {
-            if (!ts_wins) lp = x[v] - lse_all;
-            else if (v >= P.tb) lp = x[v] - lse_ts;
+        if (!tok_masked_w(P, R, mw[u], v)) {
+            if (!ts_wins) lp = xv[u] - lse_all;
+            else if (v >= P.tb) lp = xv[u] - lse_ts;
         }
-        const float sc = s.sum_lp + lp;
-        const int id = base + v;
-        if (!cand_better(sc, id, tv[MAXK2 - 1], ti[MAXK2 - 1])) continue;
-        bool placed = false;
-#pragma unroll
-        for (int j = MAXK2 - 1; j >= 0; --j) {
-            if (!placed) {
-                if (j > 0 && cand_better(sc, id, tv[j - 1], ti[j - 1])) {
-                    tv[j] = tv[j - 1];
-                    ti[j] = ti[j - 1];
-                } else {
-                    tv[j] = sc;
-                    ti[j] = id;
-                    placed = true;
-                }
-            }
-        }
+        xv[u] = s.sum_lp + lp;
+        if (v >= hi || xv[u] != xv[u]) used |= 1u << u;
     }
+    // the thread's best unused slot (score desc; ascending u = ascending flat index)
+    auto local_best = [&]() {
+        int bu = -1;
+        float bv = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < MAXK2; ++j) { lv[tid][j] = tv[j]; li[tid][j] = ti[j]; }
-    __syncthreads();
-    for (int half = 128; half >= 1; half >>= 1) {  // merge list tid + half into list tid
-        if (tid < half) {
-            float mv[MAXK2];
-            int mi[MAXK2];
-            int a = 0, b = 0;
-#pragma unroll
-            for (int j = 0; j < MAXK2; ++j) {
-                if (j < K2) {
-                    const bool ta = cand_better(lv[tid][a], li[tid][a], lv[tid + half][b], li[tid + half][b]);
-                    mv[j] = ta ? lv[tid][a] : lv[tid + half][b];
-                    mi[j] = ta ? li[tid][a] : li[tid + half][b];
-                    a += ta;
-                    b += !ta;
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < MAXK2; ++j)
-                if (j < K2) { lv[tid][j] = mv[j]; li[tid][j] = mi[j]; }
-        }
+        for (int u = 0; u < TOPK_VPT; ++u)
+            if (!((used >> u) & 1u) && (bu < 0 || xv[u] > bv)) { bv = xv[u]; bu = u; }
+        return bu < 0 ? ArgMax{-INFINITY, INT_MAX} : ArgMax{bv, base + lo + bu * 256 + tid};
+    };
+    ArgMax mine = local_best();
+    for (int r = 0; r < K2; ++r) {  // pop the block-wide best K2 times
+        ArgMax a = mine;
+        auto stp = [&](auto o) {
+            constexpr int O = decltype(o)::value;
+            a = amax(a, ArgMax{xor_lane<O>(a.v), xor_lane<O>(a.i)});
+        };
+        stp(IC<32>{}), stp(IC<16>{}), stp(IC<8>{}), stp(IC<4>{}), stp(IC<2>{}), stp(IC<1>{});
+        if ((tid & 63) == 0) red[r & 1][tid >> 6] = a;  // double-buffered: one barrier per pop
         __syncthreads();
+        ArgMax g = red[r & 1][0];
+#pragma unroll
+        for (int w = 1; w < 4; ++w) g = amax(g, red[r & 1][w]);
+        if (tid == 0) out[r] = BeamCand{g.v, g.i};
+        if (g.i != INT_MAX && mine.i == g.i) {  // flat ids are unique: one owner
+            used |= 1u << ((g.i - base - lo - tid) >> 8);
+            mine = local_best();
+        }
     }
-    if (tid < K2) out[tid] = BeamCand{lv[0][tid], li[0][tid]};
 }
 
 // grid windows, 256 threads: merge the candidates, register finished hypotheses,

@@ -584,6 +584,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nb = blockIdx.x * 64 + wave * 16;
     const int ks = blockIdx.y;
+    const int mb = blockIdx.z * ROWS;  // row group (partial mode, M > 64: beam rows)
     const int k0 = ks * kc;
     const int n = min(nb + (lane & 15), g.N - 1);
     const h16* wrow = g.W + (int64_t)n * g.ldw + k0 + 8 * (lane >> 4);
@@ -597,7 +598,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
         const int j = i * 4 + wave;
         const int row = 2 * j + (lane >> 5);
         acl[i] = ((lane & 31) ^ (row & 15)) * 8;
-        asrc[i] = grp_row(g.A, min(row, g.M - 1), g.a_grp_rows, g.a_grp_stride, g.lda) + k0;
+        asrc[i] = grp_row(g.A, min(mb + row, g.M - 1), g.a_grp_rows, g.a_grp_stride, g.lda) + k0;
     }
     auto stageA = [&](int buf, int c) {
         // a short last chunk is staged from kc-256 so every load stays inside this K range;
@@ -671,7 +672,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int m = mt * 16 + gq * 4 + i;
+            const int m = mb + mt * 16 + gq * 4 + i;
             if (m >= g.M) continue;
             if constexpr (DIRECT) store_one<EPI>(g, m, col, acc[mt][i]);
             // slabs are written through L2 (device-scope stores): no dirty lines left for
@@ -728,10 +729,12 @@ int skinny_ksplit(int N, int K) {
     return K / kc;
 }
 
-// partial-slab mode: always writes part[ks][M][N] (no epilogue); returns ksplit
+// partial-slab mode: always writes part[ks][M][N] (no epilogue); returns ksplit.
+// M > 64 (beam rows) runs ceil(M / 64) row groups on grid z; they read the same
+// weights, so the weight stream comes from HBM once and from the MALL/L2 after.
 int launch_gemm_skinny_partial(const GemmArgs& g, float* part, hipStream_t s) {
     const int ks = skinny_ksplit(g.N, g.K);
-    const dim3 grid((g.N + 63) / 64, ks);
+    const dim3 grid((g.N + 63) / 64, ks, (g.M + 63) / 64);
     const int kc = g.K / ks;
     switch ((g.M + 15) / 16) {
         case 1: gemm_skinny_kernel<1, false, EPI_F32><<<grid, 256, 0, s>>>(g, kc, part); break;

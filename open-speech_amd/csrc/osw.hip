@@ -433,10 +433,11 @@ void setup_workspace(osw_ctx* c) {
     c->sel_arrive = dalloc<int>(1, o);
     HIPCHK(hipMemset(c->sel_arrive, 0, sizeof(int)));
     {
-        const int64_t Bm = std::min<int64_t>(R, 64);
         const int64_t shapes[][2] = {{3 * Dd, Dd}, {Dd, Dd}, {4 * Dd, Dd}, {Dd, 4 * Dd}, {d.n_vocab, Dd}};
-        for (auto& nk : shapes)
-            c->part_floats = std::max<int64_t>(c->part_floats, skinny_ksplit((int)nk[0], (int)nk[1]) * Bm * nk[0]);
+        for (auto& nk : shapes)  // skinny split-K slabs: decoder projections at any row count
+            c->part_floats = std::max<int64_t>(c->part_floats,
+                                               skinny_ksplit((int)nk[0], (int)nk[1]) * nk[0] *
+                                                   (nk[0] == d.n_vocab ? std::min<int64_t>(R, 64) : R));
         for (auto& nk : shapes)  // > 64 rows: split-K slabs of the tiled GEMM
             if (R > 64 && nk[0] != d.n_vocab)
                 c->part_floats = std::max<int64_t>(c->part_floats,
@@ -562,9 +563,12 @@ void decoder_step(osw_ctx* c, int nb, int group, bool gather) {
     const int64_t kv_layer = (int64_t)nb * H * ctx * 64;
     REQUIRE(nb <= c->R && D <= 1280, "decoder step: rows <= capacity and D <= 1280");
     REQUIRE(ctx <= 448, "decoder self-attention holds at most 448 positions");
-    // <= 64 rows: split-K skinny GEMM; more (beam search): one slab from the tiled GEMM
+    // <= 64 rows: split-K skinny GEMM; more (beam search): see below
     auto partial = [&](const h16* A, int lda, const h16* Wt, int N, int K) {
-        if (nb > 64) {
+        // > 64 rows, N > 1536: 128x128 split-K tiles; N <= 1536: skinny row groups (measured
+        // at 320 rows: N = 1280 11.4 vs 12.8 us, N = 3840 17.9 vs 12.8, N = 5120 21.7 vs 20.4)
+        static const int force = getenv("OSW_BEAM_GEMM") ? atoi(getenv("OSW_BEAM_GEMM")) : 0;  // 1 tiled, 2 skinny
+        if (nb > 64 && (force == 1 || (force == 0 && N > 1536))) {
             const int ks = tiled_ksplit(nb, N, K);
             REQUIRE((int64_t)ks * nb * N <= c->part_floats, "decoder workspace too small");
             launch_gemm_tiled_partial(gemm_plain(A, lda, Wt, nullptr, nb, N, K, nullptr, 0, EPI_F32), c->part, ks,

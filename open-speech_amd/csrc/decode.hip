@@ -38,6 +38,12 @@ __device__ __forceinline__ float block_reduce_sum(float v, float* red) {
     return r;
 }
 
+template <bool NT>
+__device__ __forceinline__ h16x8 ld8(const h16* p) {
+    if constexpr (NT) return __builtin_nontemporal_load((const h16x8*)p);
+    return *(const h16x8*)p;
+}
+
 // Attention of one query row over n_keys rows of K/V ([n][64] fp16, contiguous);
 // K/V loads are nontemporal (the self-K/V caches of a step exceed the MALL): 18.7 -> 17.1 us.
 // 256 threads.  Scores live in LDS (n_keys <= MAXK).  Loads are issued in groups
@@ -47,7 +53,7 @@ __device__ __forceinline__ float block_reduce_sum(float v, float* red) {
 // GATHER (beam search): key p of this row lives in the cache slot of the row that
 // wrote position p of this hypothesis' history: K + soff[p] * slot_stride, where
 // soff[p] = anc[p] - self (staged in LDS; the newest key is always this row's own).
-template <int MAXK, bool GATHER = false>
+template <int MAXK, bool GATHER = false, bool NT = !GATHER>
 __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ K, const h16* __restrict__ V,
                            int n_keys, h16* __restrict__ out, const int* __restrict__ anc = nullptr, int self = 0,
                            int64_t slot_stride = 0) {
@@ -79,7 +85,7 @@ __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ 
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int key = min(base + u * 32 + w * 8 + kr, n_keys - 1);
-            kv[u] = __builtin_nontemporal_load((const h16x8*)(krow(K, key) + 8 * c8));
+            kv[u] = ld8<NT>(krow(K, key) + 8 * c8);
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -113,7 +119,7 @@ __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ 
         h16x8 v[8];
         float p[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load((const h16x8*)(krow(V, j + 32 * u) + 8 * c));
+        for (int u = 0; u < 8; ++u) v[u] = ld8<NT>(krow(V, j + 32 * u) + 8 * c);
 #pragma unroll
         for (int u = 0; u < 8; ++u) p[u] = sc[j + 32 * u];
 #pragma unroll
@@ -122,7 +128,7 @@ __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ 
             for (int e = 0; e < 8; ++e) acc[e] = fmaf(p[u], (float)v[u][e], acc[e]);
     }
     for (; j < n_keys; j += 32) {
-        const h16x8 v = __builtin_nontemporal_load((const h16x8*)(krow(V, j) + 8 * c));
+        const h16x8 v = ld8<NT>(krow(V, j) + 8 * c);
         const float p = sc[j];
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[e] = fmaf(p, (float)v[e], acc[e]);
@@ -165,10 +171,23 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
                                                             const float* __restrict__ bias, h16* __restrict__ kcache,
                                                             h16* __restrict__ vcache, const int* __restrict__ pos_ptr,
                                                             int H, int B, int ctx, h16* __restrict__ out,
-                                                            const int* __restrict__ anc) {
+                                                            const int* __restrict__ anc, int group) {
     __shared__ h16 q16[HD];
     __shared__ float red4[256];
-    const int h = blockIdx.x, b = blockIdx.y;
+    int h, b;
+    if (anc) {
+        // beam rows: the `group` hypotheses of one (window, head) run adjacently on one
+        // XCD, so the cache rows they share through the ancestry table hit that L2
+        const int nwg = gridDim.x, bid = blockIdx.x;
+        const int qq = nwg / 8, rr = nwg % 8, xcd = bid % 8;
+        const int lin = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + bid / 8;
+        const int k = lin % group, w = lin / (group * H);
+        h = (lin / group) % H;
+        b = w * group + k;
+    } else {
+        h = blockIdx.x % H;
+        b = blockIdx.x / H;
+    }
     const int D = H * HD;
     const int pos = min(*pos_ptr, ctx - 1);  // graph replays may run past max_length on finished windows
     h16* kc = kcache + ((int64_t)b * H + h) * ctx * HD;
@@ -337,30 +356,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
         }
     }
     __syncthreads();
-    if (wv != 0) return;
-    // publish this chunk's partials with device-scope (write-through) stores, wait for
-    // them, then take the (window, head) arrival ticket: the 8th arriver merges
+    __shared__ int last;
+    if (wv == 0) {
+        // publish this chunk's partials with device-scope (write-through) stores, wait for
+        // them, then take the (window, head) arrival ticket: the 8th arriver merges
 #pragma unroll
-    for (int k = 0; k < NB; ++k) {
-        if (k >= beam) break;
-        float* dst = ws + (((int64_t)(r0 + k) * H + h) * XCH + chunk) * XPART;
-        const float a = (red[0][k][lane] + red[1][k][lane]) + (red[2][k][lane] + red[3][k][lane]);
-        const float l = (rl[0][k] + rl[1][k]) + (rl[2][k] + rl[3][k]);
-        __hip_atomic_store(dst + 4 + lane, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int k = 0; k < NB; ++k) {
+            if (k >= beam) break;
+            float* dst = ws + (((int64_t)(r0 + k) * H + h) * XCH + chunk) * XPART;
+            const float a = (red[0][k][lane] + red[1][k][lane]) + (red[2][k][lane] + red[3][k][lane]);
+            const float l = (rl[0][k] + rl[1][k]) + (rl[2][k] + rl[3][k]);
+            __hip_atomic_store(dst + 4 + lane, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) {
+                __hip_atomic_store(dst, mx[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(dst + 1, l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0);  // the stores above are complete at device scope
+        int old = 0;
+        if (lane == 0) old = __hip_atomic_fetch_add(ticket + p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        old = __builtin_amdgcn_readfirstlane(old);
         if (lane == 0) {
-            __hip_atomic_store(dst, mx[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(dst + 1, l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = old == XCH - 1;
+            if (old == XCH - 1) __hip_atomic_store(ticket + p, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    __builtin_amdgcn_s_waitcnt(0);  // the stores above are complete at device scope
-    int old = 0;
-    if (lane == 0) old = __hip_atomic_fetch_add(ticket + p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    old = __builtin_amdgcn_readfirstlane(old);
-    if (old != XCH - 1) return;
-    if (lane == 0) __hip_atomic_store(ticket + p, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+    if (NB == 1 && wv != 0) return;  // one row: wave 0 merges alone
+    __syncthreads();
+    if (!last) return;
     // merge in fixed chunk order: out = Σ e^(m_s - M) acc_s / Σ e^(m_s - M) l_s (device-scope
-    // loads: the other chunks' partials may come from another XCD's writes)
-    for (int k = 0; k < beam; ++k) {
+    // loads: the other chunks' partials may come from another XCD's writes); beam rows
+    // are spread over the 4 waves so their load round trips overlap
+    for (int k = wv; k < beam; k += 4) {
         const float* src = ws + ((int64_t)(r0 + k) * H + h) * XCH * XPART;
         float mm[XCH];
         float M = -INFINITY;
@@ -976,8 +1003,8 @@ int sel_parts_bytes() { return (int)sizeof(SelPart) * SEL_SPLIT; }
 int beam_cand_bytes(int beam) { return (int)sizeof(BeamCand) * BEAM_SLICES * 2 * beam; }
 
 void launch_dec_self_attn(const float* part, int ks, const float* bias, h16* kc, h16* vc, const int* pos, int B,
-                          int H, int ctx, h16* out, const int* anc, hipStream_t s) {
-    dec_self_attn_kernel<<<dim3(H, B), 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, anc);
+                          int H, int ctx, h16* out, const int* anc, int group, hipStream_t s) {
+    dec_self_attn_kernel<<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, anc, anc ? group : 1);
 }
 
 void launch_dec_cross_attn(const float* part, int ks, const float* bias, const h16* xk, const h16* xv, int B, int H,

@@ -33,7 +33,7 @@ void launch_enc_attn(const h16*, h16*, int, int, int, hipStream_t);
 void launch_init_uniform(void*, bool, int64_t, uint64_t, float, float, int64_t, int64_t, hipStream_t);
 uint64_t hash_stream_key(uint64_t, int64_t);
 void launch_dec_embed(const h16*, const float*, const int*, const int*, int, int, int, float*, hipStream_t);
-void launch_dec_self_attn(const float*, int, const float*, h16*, h16*, const int*, int, int, int, h16*, const int*,
+void launch_dec_self_attn(const float*, int, const float*, h16*, h16*, const int*, int, int, int, h16*, const int*, int,
                           hipStream_t);
 void launch_dec_cross_attn(const float*, int, const float*, const h16*, const h16*, int, int, int, int, h16*, float*,
                            int*, hipStream_t);
@@ -586,7 +586,7 @@ void decoder_step(osw_ctx* c, int nb, int group, bool gather) {
         const std::string p = "dec.l" + std::to_string(l);
         int ks = partial(c->xdn, D, WH(c, p + ".qkv.w"), 3 * D, D);
         launch_dec_self_attn(c->part, ks, WF(c, p + ".qkv.b"), c->kc + l * kv_layer, c->vc + l * kv_layer, c->pos, nb,
-                             H, ctx, c->dattn, gather ? c->anc : nullptr, c->stream);
+                             H, ctx, c->dattn, gather ? c->anc : nullptr, group, c->stream);
         ks = partial(c->dattn, D, WH(c, p + ".o.w"), D, D);
         launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".o.b"), c->xd, WF(c, p + ".ln2.g"), WF(c, p + ".ln2.b"),
                             c->xdn, nullptr, nullptr, nullptr, nullptr, ctx, c->stream);

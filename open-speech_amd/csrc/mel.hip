@@ -21,9 +21,16 @@
 namespace osw {
 
 namespace {
-constexpr int FPB = 16;          // frames per block
+constexpr int FPB = 16;          // frames per block (stage 2 maps FPB x 16 onto the 256 threads)
 constexpr int NFFT = 400, HOP = 160, NBIN = 201;
 constexpr int SPAN = HOP * (FPB - 1) + NFFT;  // 2800 samples
+
+// w16^j = w400^(25 j) and w25^j = w400^(16 j), the host table's float values as
+// constants (indices are compile-time after unrolling: immediates, no LDS reads)
+constexpr float W16R[16] = {1.0f, 0.9238795042037964f, 0.7071067690849304f, 0.3826834261417389f, 6.123234262925839e-17f, -0.3826834261417389f, -0.7071067690849304f, -0.9238795042037964f, -1.0f, -0.9238795042037964f, -0.7071067690849304f, -0.3826834261417389f, -1.8369701465288538e-16f, 0.3826834261417389f, 0.7071067690849304f, 0.9238795042037964f};
+constexpr float W16I[16] = {-0.0f, -0.3826834261417389f, -0.7071067690849304f, -0.9238795042037964f, -1.0f, -0.9238795042037964f, -0.7071067690849304f, -0.3826834261417389f, -1.2246468525851679e-16f, 0.3826834261417389f, 0.7071067690849304f, 0.9238795042037964f, 1.0f, 0.9238795042037964f, 0.7071067690849304f, 0.3826834261417389f};
+constexpr float W25R[25] = {1.0f, 0.9685831665992737f, 0.8763066530227661f, 0.728968620300293f, 0.5358268022537231f, 0.30901700258255005f, 0.06279052048921585f, -0.187381312251091f, -0.4257792830467224f, -0.6374239921569824f, -0.80901700258255f, -0.9297764897346497f, -0.9921147227287292f, -0.9921147227287292f, -0.9297764897346497f, -0.80901700258255f, -0.6374239921569824f, -0.4257792830467224f, -0.187381312251091f, 0.06279052048921585f, 0.30901700258255005f, 0.5358268022537231f, 0.728968620300293f, 0.8763066530227661f, 0.9685831665992737f};
+constexpr float W25I[25] = {-0.0f, -0.24868988990783691f, -0.4817536771297455f, -0.6845471262931824f, -0.8443279266357422f, -0.9510565400123596f, -0.9980267286300659f, -0.9822872281074524f, -0.9048270583152771f, -0.7705132365226746f, -0.5877852439880371f, -0.3681245446205139f, -0.12533323466777802f, 0.12533323466777802f, 0.3681245446205139f, 0.5877852439880371f, 0.7705132365226746f, 0.9048270583152771f, 0.9822872281074524f, 0.9980267286300659f, 0.9510565400123596f, 0.8443279266357422f, 0.6845471262931824f, 0.4817536771297455f, 0.24868988990783691f};
 
 __device__ __forceinline__ int64_t reflect_idx(int64_t j, int64_t L) {
     if (L <= 1) return 0;
@@ -59,9 +66,13 @@ __global__ __launch_bounds__(256) void mel_logmel_kernel(
         win[i] = hann[i];
     }
     const int64_t j0 = (int64_t)t0 * HOP - NFFT / 2;
-    for (int i = tid; i < SPAN; i += 256) {
-        const int64_t jj = reflect_idx(j0 + i, L);
-        xs[i] = jj < N ? (float)pcm[base + jj] * (1.0f / 32768.0f) : 0.0f;
+    if (j0 >= 0 && j0 + SPAN <= N) {  // interior block: no reflection, no padding
+        for (int i = tid; i < SPAN; i += 256) xs[i] = (float)pcm[base + j0 + i] * (1.0f / 32768.0f);
+    } else {
+        for (int i = tid; i < SPAN; i += 256) {
+            const int64_t jj = reflect_idx(j0 + i, L);
+            xs[i] = jj < N ? (float)pcm[base + jj] * (1.0f / 32768.0f) : 0.0f;
+        }
     }
     __syncthreads();
 
@@ -80,9 +91,8 @@ __global__ __launch_bounds__(256) void mel_logmel_kernel(
             float re = 0.f, im = 0.f;
 #pragma unroll
             for (int n1 = 0; n1 < 16; ++n1) {
-                const float2 w = tw[((n1 * k1) & 15) * 25];  // w16^(n1 k1) = w400^(25 n1 k1)
-                re = fmaf(v[n1], w.x, re);
-                im = fmaf(v[n1], w.y, im);
+                re = fmaf(v[n1], W16R[(n1 * k1) & 15], re);  // w16^(n1 k1)
+                im = fmaf(v[n1], W16I[(n1 * k1) & 15], im);
             }
             Y[k1] = make_float2(re, im);
         }
@@ -95,34 +105,52 @@ __global__ __launch_bounds__(256) void mel_logmel_kernel(
     }
     __syncthreads();
 
-    // stage 2: X[k1 + 16 k2] = sum_n2 Z[n2][k1] w25^(n2 k2); power spectrum
-    for (int task = tid; task < FPB * NBIN; task += 256) {
-        const int f = task / NBIN, k = task % NBIN;
-        const int k1 = k & 15, k2 = k >> 4;
-        float re = 0.f, im = 0.f;
-#pragma unroll 5
-        for (int n2 = 0; n2 < 25; ++n2) {
-            const float2 z = Z[f][n2][k1];
-            const float2 w = tw[((n2 * k2) % 25) * 16];  // w25^(n2 k2) = w400^(16 n2 k2)
-            re += z.x * w.x - z.y * w.y;
-            im += z.x * w.y + z.y * w.x;
+    // stage 2: X[k1 + 16 k2] = sum_n2 Z[n2][k1] w25^(n2 k2); power spectrum.  One
+    // thread per (frame, k1): its 25 Z values are read once and feed all k2 (<= 13).
+    {
+        const int f = tid >> 4, k1 = tid & 15;  // FPB * 16 == 256 threads
+        float2 z[25];
+#pragma unroll
+        for (int n2 = 0; n2 < 25; ++n2) z[n2] = Z[f][n2][k1];
+#pragma unroll
+        for (int k2 = 0; k2 < 13; ++k2) {
+            const int k = k1 + 16 * k2;
+            if (k < NBIN) {
+                float re = 0.f, im = 0.f;
+#pragma unroll
+                for (int n2 = 0; n2 < 25; ++n2) {
+                    const float wr = W25R[(n2 * k2) % 25], wi = W25I[(n2 * k2) % 25];
+                    re += z[n2].x * wr - z[n2].y * wi;
+                    im += z[n2].x * wi + z[n2].y * wr;
+                }
+                P[f][k] = re * re + im * im;
+            }
         }
-        P[f][k] = re * re + im * im;
     }
     __syncthreads();
 
-    // stage 3: mel, log10; time-major store; block max
+    // stage 3: mel, log10; time-major store; block max.  Thread = (mel m, half of the
+    // frames): the filter's weights are read once for 8 frames.
     float lmax = -INFINITY;
-    for (int task = tid; task < FPB * n_mels; task += 256) {
-        const int f = task / n_mels, m = task % n_mels;
-        const int t = t0 + f;
-        if (t >= nf) continue;
+    for (int task = tid; task < 2 * n_mels; task += 256) {
+        const int m = task % n_mels, f0 = (task / n_mels) * (FPB / 2);
         const int lo = flo[m], cnt = fcnt[m], off = foff[m];
-        float s = 0.f;
-        for (int i = 0; i < cnt; ++i) s = fmaf(fw[off + i], P[f][lo + i], s);
-        const float lg = log10f(fmaxf(s, 1e-10f));
-        logmel[mel_off[clip] + (int64_t)t * n_mels + m] = lg;
-        lmax = fmaxf(lmax, lg);
+        float s[FPB / 2];
+#pragma unroll
+        for (int j = 0; j < FPB / 2; ++j) s[j] = 0.f;
+        for (int i = 0; i < cnt; ++i) {
+            const float wgt = fw[off + i];
+#pragma unroll
+            for (int j = 0; j < FPB / 2; ++j) s[j] = fmaf(wgt, P[f0 + j][lo + i], s[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < FPB / 2; ++j) {
+            const int t = t0 + f0 + j;
+            if (t >= nf) break;
+            const float lg = log10f(fmaxf(s[j], 1e-10f));
+            logmel[mel_off[clip] + (int64_t)t * n_mels + m] = lg;
+            lmax = fmaxf(lmax, lg);
+        }
     }
     lmax = wave_max(lmax);
     if ((tid & 63) == 0) red[tid >> 6] = lmax;

@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--latency-repeats", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--beam5", type=int, default=1, help="also time one isolated beam-5 step (the reference default)")
+    ap.add_argument("--beam5-steps", type=int, default=3,
+                    help="also time this many beam-5 steps on the lanes (after the greedy timed region)")
     ap.add_argument("--cpu-decode-steps", type=int, default=8)
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc.json"),
                     help="per-kernel HBM bytes from a rocprofv3 --pmc pass (tools/pmc_summary.py)")
@@ -161,6 +163,31 @@ def main():
     value = audio_s / el
     tokens_per_clip = ntok / (n_total * a.steps)
 
+    # The reference's own decoding (beam_size=5, src/backends/faster_whisper.py:237) on the
+    # same lanes: warm-up steps let every lane capture its beam graph, then K_b timed steps.
+    beam5_lanes = None
+    if a.beam5_steps > 0:
+        dp.cfg = DecodeConfig(suppress_tokens=sup, max_length=a.max_length, beam_size=5)
+        dp.run_steps(allpcm, len(dp.lanes))
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        tb0 = time.perf_counter()
+        bres = dp.run_steps(allpcm, a.beam5_steps)
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        bel = time.perf_counter() - tb0
+        if dist:
+            t = torch.tensor([bel], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            bel = float(t.item())
+        btok = sum(len(o.tokens) for outs, _ in bres for o in outs) / (B * a.beam5_steps)
+        beam5_lanes = {"value": round(n_total * a.beam5_steps * 30.0 / bel, 2), "unit": "audio-sec/sec",
+                       "steps": a.beam5_steps, "ms_per_step": round(bel / a.beam5_steps * 1e3, 2),
+                       "lanes_per_gpu": len(dp.lanes), "tokens_per_clip": round(btok, 1)}
+        dp.cfg = cfg
+
     if rank == 0:
         # Roofline pass, after the timed region: lane 0 alone runs one more step of the
         # same workload with per-kernel HIP-event timers on its stream and the decode
@@ -240,6 +267,7 @@ def main():
                        "lanes_per_gpu": len(dp.lanes)},
             "tokens_per_clip": round(tokens_per_clip, 1),
             "p50_latency_ms_b1": None if p50 is None else round(p50, 2),
+            "beam5": beam5_lanes,
             "beam5_audio_sec_per_sec_1lane": beam5,
             "realtime_factor": round(value, 1),
             "roofline": roof,

@@ -682,6 +682,98 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
         }
 }
 
+// Wide-N, few-row GEMM (decoder logits: M <= 64 rows x 51866 vocabulary columns,
+// K = d_model): the weights (133 MB at turbo) are streamed once per step and the
+// few activation rows are re-read from L2.  Tile 64 rows x 128 columns, 4 waves of
+// 64 x 32; a 3-slot LDS ring keeps two 64-deep K tiles in flight per workgroup
+// (72 KB -> 2 workgroups per CU, so the 406 tiles of the vocabulary are resident at
+// once), where the generic 128x128 kernel keeps one and waits a full HBM round trip
+// per K tile.  fp32 out, written through L2 (device-scope stores) for the select
+// kernels.
+constexpr int WBM = 64, WBN = 128, WSL = 3;
+__global__ __launch_bounds__(256, 2) void gemm_wide_kernel(GemmArgs g) {
+    __shared__ __attribute__((aligned(16))) h16 la[WSL][WBM * BK];
+    __shared__ __attribute__((aligned(16))) h16 lw[WSL][WBN * BK];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int n0 = blockIdx.x * WBN;
+    // staging: one wave-instruction fills 8 rows x 64 k (1 KiB); A 8 groups (2 per
+    // wave), W 16 groups (4 per wave); the 16-B chunk is XOR-swizzled by row
+    const h16* asrc[2];
+    const h16* wsrc[4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int r = (i * 4 + wave) * 8 + (lane >> 3);
+        asrc[i] = g.A + (int64_t)min(r, g.M - 1) * g.lda + swz(r, lane & 7) * 8;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = (i * 4 + wave) * 8 + (lane >> 3);
+        wsrc[i] = g.W + (int64_t)min(n0 + r, g.N - 1) * g.ldw + swz(r, lane & 7) * 8;
+    }
+    auto stage = [&](int slot, int k0) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + k0), (OSW_LDS void*)&la[slot][(i * 4 + wave) * 8 * BK],
+                                             16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + k0), (OSW_LDS void*)&lw[slot][(i * 4 + wave) * 8 * BK],
+                                             16, 0, 0);
+    };
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nk = g.K / BK;
+    stage(0, 0);
+    if (nk > 1) stage(1, BK);
+    for (int kt = 0; kt < nk; ++kt) {
+        if (kt + 1 < nk)
+            wait_vmcnt<6>();  // this thread's tile kt has landed; tile kt+1 stays in flight
+        else
+            wait_vmcnt<0>();
+        __syncthreads();  // every thread's tile kt has landed; slot (kt+2)%3 is no longer read
+        if (kt + 2 < nk) stage((kt + 2) % WSL, (kt + 2) * BK);
+        const h16* A = la[kt % WSL];
+        const h16* W = lw[kt % WSL];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int c = ks * 4 + (lane >> 4);
+            h16x8 a[4], b[2];
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) {
+                const int row = mi * 16 + (lane & 15);
+                a[mi] = *(const h16x8*)&A[row * BK + swz(row, c) * 8];
+            }
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) {
+                const int row = wave * 32 + ni * 16 + (lane & 15);
+                b[ni] = *(const h16x8*)&W[row * BK + swz(row, c) * 8];
+            }
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 2; ++ni)
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int m = mi * 16 + (lane >> 4) * 4 + i;
+            if (m >= g.M) continue;
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) {
+                const int n = n0 + wave * 32 + ni * 16 + (lane & 15);
+                if (n >= g.N) continue;
+                const float v = g.bias ? acc[mi][ni][i] + g.bias[n] : acc[mi][ni][i];
+                __hip_atomic_store((float*)g.C + (int64_t)m * g.ldc + n, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+}
+
 template <int EPI>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g, int ksplit, const float* __restrict__ part) {
     const int64_t total = (int64_t)g.M * g.N;
@@ -788,6 +880,13 @@ void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s);
 void launch_gemm(const GemmArgs& g, hipStream_t s) { launch_gemm_variant(g, 0, s); }
 
 void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s) {
+    // few rows, very wide N, plain fp32 out (decoder logits): the 3-slot ring kernel
+    static const bool no_wide = getenv("OSW_NO_WIDE") != nullptr;  // A/B switch
+    const bool wide_ok = g.M <= WBM && g.epi == EPI_F32 && g.kc == 0 && g.c_grp_rows == g.M && g.K % BK == 0;
+    if (wide_ok && (variant == 5 || (variant == 0 && g.N >= 16384 && !no_wide))) {
+        gemm_wide_kernel<<<(g.N + WBN - 1) / WBN, 256, 0, s>>>(g);
+        return;
+    }
     // big tile when it still yields >= 2 waves of workgroups over 256 CUs
     const int64_t big_tiles = (int64_t)((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
     const bool big = variant == 2 || (variant == 0 && big_tiles >= 512 && g.N % 8 == 0 && !getenv("OSW_GEMM128"));

@@ -22,7 +22,8 @@ def eng():
     (1, 300, 200, 128), (1, 1500, 1280, 1280), (2, 1000, 700, 192), (2, 2048, 1280, 640), (4, 1000, 700, 192),
     (4, 2048, 1280, 640), (4, 700, 300, 64), (4, 513, 1000, 128), (4, 3000, 2304, 1280), (2, 777, 264, 128),
     (3, 1, 1280, 1280), (3, 7, 51866, 384), (3, 64, 5120, 1280), (3, 33, 1280, 5120), (0, 5, 300, 256),
-    (3, 64, 51866, 1280), (3, 16, 384, 1536), (3, 3, 700, 128), (3, 50, 40000, 640)])
+    (3, 64, 51866, 1280), (3, 16, 384, 1536), (3, 3, 700, 128), (3, 50, 40000, 640),
+    (5, 64, 51866, 1280), (5, 1, 51866, 1280), (5, 37, 20000, 384), (5, 64, 300, 64), (5, 5, 1000, 128)])
 def test_gemm_variants(eng, variant, M, N, K):
     rng = np.random.default_rng(M * 7 + N)
     A = rng.uniform(-1, 1, (M, K)).astype(np.float16)

@@ -577,14 +577,31 @@ __device__ __forceinline__ float gumbel_noise(unsigned long long seed, int row, 
     return -logf(-logf(u));
 }
 
-// grid (B, SEL_SPLIT), 256 threads
-__global__ __launch_bounds__(256) void select_partial_kernel(const float* __restrict__ logits, SelParams P,
-                                                             const int* __restrict__ pos_ptr,
-                                                             const unsigned* __restrict__ supmask,
-                                                             const SelState* __restrict__ st,
-                                                             SelPart* __restrict__ parts) {
+// Slice partials are published with device-scope stores (they write through the
+// XCD's L2) and read back with device-scope loads by the row's finaliser, which may
+// run on another XCD.
+__device__ __forceinline__ void store_part(SelPart* dst, const SelPart& r) {
+    float* f = (float*)dst;
+    const float* v = (const float*)&r;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(SelPart) / 4); ++i)
+        __hip_atomic_store(f + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ SelPart load_part(const SelPart* src) {
+    SelPart r;
+    float* v = (float*)&r;
+    const float* f = (const float*)src;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(SelPart) / 4); ++i)
+        v[i] = __hip_atomic_load(f + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return r;
+}
+
+// grid (B, SEL_SPLIT), 256 threads: one vocabulary slice of one row
+__device__ __forceinline__ void select_partial_body(const float* __restrict__ logits, const SelParams& P, int step,
+                                                    const unsigned* __restrict__ supmask,
+                                                    const SelState* __restrict__ st, SelPart* __restrict__ parts) {
     const int b = blockIdx.x, sl = blockIdx.y, tid = threadIdx.x;
-    const int step = *pos_ptr;
     const SelState s = st[b];
     const int mode = sel_mode(P, step, s);
     if (mode == SEL_PROMPT || mode == SEL_DONE) return;
@@ -638,14 +655,14 @@ __global__ __launch_bounds__(256) void select_partial_kernel(const float* __rest
             ArgMax T = amax(ArgMax{r.v_ts, r.i_ts}, ArgMax{q.v_ts, q.i_ts});
             r.v_all = A.v; r.i_all = A.i; r.v_text = X.v; r.i_text = X.i; r.v_ts = T.v; r.i_ts = T.i;
         }
-        parts[b * SEL_SPLIT + sl] = r;
+        store_part(parts + b * SEL_SPLIT + sl, r);
     }
 }
 
 __device__ __forceinline__ SelPart combine_parts(const SelPart* __restrict__ parts) {
-    SelPart r = parts[0];
+    SelPart r = load_part(parts);
     for (int i = 1; i < SEL_SPLIT; ++i) {
-        const SelPart& q = parts[i];
+        const SelPart q = load_part(parts + i);
         lse_merge(r.m_all, r.s_all, q.m_all, q.s_all);
         lse_merge(r.m_ts, r.s_ts, q.m_ts, q.s_ts);
         ArgMax A = amax(ArgMax{r.v_all, r.i_all}, ArgMax{q.v_all, q.i_all});
@@ -716,25 +733,32 @@ __device__ __forceinline__ void select_final_row(const float* __restrict__ logit
     cur_tok[b] = next;
 }
 
-// grid rows, 64 threads (thread 0 works): the greedy choice for each row.  With
-// `bump` (greedy steps) the last row to finish advances the device step counter, so
-// no separate launch is needed; every row read the counter before it arrived.
-__global__ __launch_bounds__(64) void select_final_kernel(const float* __restrict__ logits, SelParams P,
-                                                          int* __restrict__ pos_ptr,
-                                                          const int* __restrict__ prompt,  // [B][P] (-1 = detect)
-                                                          const SelPart* __restrict__ parts,
-                                                          SelState* __restrict__ st, int* __restrict__ cur_tok,
-                                                          int* __restrict__ tokens, int max_tokens,
-                                                          int* __restrict__ arrive, int bump) {
-    if (threadIdx.x != 0) return;
+// grid (rows, SEL_SPLIT), 256 threads: every slice of a row computes its partial
+// and takes the row's arrival ticket (also slices that have nothing to do, so the
+// finaliser knows every slice has read the step counter); the last one combines the
+// slices in fixed order and picks the row's token (select_final_row).  With `bump`
+// (greedy steps) the last row to be finalised advances the device step counter: by
+// then every slice of every row has read it.  One launch instead of partial + final.
+__global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ logits, SelParams P,
+                                                     int* __restrict__ pos_ptr, const unsigned* __restrict__ supmask,
+                                                     const int* __restrict__ prompt, SelPart* __restrict__ parts,
+                                                     SelState* __restrict__ st, int* __restrict__ cur_tok,
+                                                     int* __restrict__ tokens, int max_tokens,
+                                                     int* __restrict__ arrive, int* __restrict__ ticket, int bump) {
     const int step = *pos_ptr;
+    select_partial_body(logits, P, step, supmask, st, parts);
+    if (threadIdx.x != 0) return;
+    __builtin_amdgcn_s_waitcnt(0);  // this slice's part stores are complete at device scope
+    const int b = blockIdx.x;
+    if (__hip_atomic_fetch_add(ticket + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != SEL_SPLIT - 1) return;
+    __hip_atomic_store(ticket + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
     select_final_row(logits, P, step, prompt, parts, st, cur_tok, tokens, max_tokens);
     if (!bump) return;
+    __builtin_amdgcn_s_waitcnt(0);
     if (__hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
         __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(pos_ptr, step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-
 }
 
 // ---------------------------------------------------------------------------
@@ -1041,9 +1065,9 @@ void launch_dec_reduce_gelu(const float* part, int ks, int B, int N, const float
 void launch_select(const float* logits, int rows, int* pos, const SelParams& P, const int* prompt,
                    const unsigned* supmask, SelState* st, int* cur_tok, int* tokens, int max_tokens, void* sel_parts,
                    int* arrive, bool bump, hipStream_t s) {
-    select_partial_kernel<<<dim3(rows, SEL_SPLIT), 256, 0, s>>>(logits, P, pos, supmask, st, (SelPart*)sel_parts);
-    select_final_kernel<<<rows, 64, 0, s>>>(logits, P, pos, prompt, (const SelPart*)sel_parts, st, cur_tok, tokens,
-                                             max_tokens, arrive, bump ? 1 : 0);
+    // arrive[0]: rows finalised this step; arrive[1 + row]: the row's slice tickets
+    select_kernel<<<dim3(rows, SEL_SPLIT), 256, 0, s>>>(logits, P, pos, supmask, prompt, (SelPart*)sel_parts, st,
+                                                        cur_tok, tokens, max_tokens, arrive, arrive + 1, bump ? 1 : 0);
 }
 
 void launch_beam(const float* logits, int windows, const int* pos, const SelParams& P, const unsigned* supmask,

@@ -162,7 +162,7 @@ struct osw_ctx {
     float* part = nullptr;     // split-K partial slabs of the decoder GEMMs
     float* xws = nullptr;      // cross-attention per-chunk partials [R][H][XCHUNKS][XPART]
     int* xticket = nullptr;    // cross-attention arrival tickets [B][H] (zero between launches)
-    int* sel_arrive = nullptr; // select_final arrival counter (zero between launches)
+    int* sel_arrive = nullptr; // select arrival counters: rows finalised + per-row slice tickets (zero between launches)
     int64_t part_floats = 0;
 
     // decode-step graph (CH steps per replay), re-captured when its key changes
@@ -430,8 +430,8 @@ void setup_workspace(osw_ctx* c) {
     c->xws = dalloc<float>(R * d.n_text_head * XCHUNKS * XPART, o);
     c->xticket = dalloc<int>(B * d.n_text_head, o);
     HIPCHK(hipMemset(c->xticket, 0, (size_t)B * d.n_text_head * sizeof(int)));
-    c->sel_arrive = dalloc<int>(1, o);
-    HIPCHK(hipMemset(c->sel_arrive, 0, sizeof(int)));
+    c->sel_arrive = dalloc<int>(1 + R, o);  // [0] rows finalised, [1 + row] slice tickets
+    HIPCHK(hipMemset(c->sel_arrive, 0, (1 + (size_t)R) * sizeof(int)));
     {
         const int64_t shapes[][2] = {{3 * Dd, Dd}, {Dd, Dd}, {4 * Dd, Dd}, {Dd, 4 * Dd}, {d.n_vocab, Dd}};
         for (auto& nk : shapes)  // skinny split-K slabs: decoder projections at any row count

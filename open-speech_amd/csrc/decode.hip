@@ -659,10 +659,13 @@ __device__ __forceinline__ void select_partial_body(const float* __restrict__ lo
     }
 }
 
+// DEVICE: the slices were written by other workgroups of the same launch (device-scope
+// loads); otherwise by an earlier launch (plain loads).
+template <bool DEVICE>
 __device__ __forceinline__ SelPart combine_parts(const SelPart* __restrict__ parts) {
-    SelPart r = load_part(parts);
+    SelPart r = DEVICE ? load_part(parts) : parts[0];
     for (int i = 1; i < SEL_SPLIT; ++i) {
-        const SelPart q = load_part(parts + i);
+        const SelPart q = DEVICE ? load_part(parts + i) : parts[i];
         lse_merge(r.m_all, r.s_all, q.m_all, q.s_all);
         lse_merge(r.m_ts, r.s_ts, q.m_ts, q.s_ts);
         ArgMax A = amax(ArgMax{r.v_all, r.i_all}, ArgMax{q.v_all, q.i_all});
@@ -692,7 +695,7 @@ __device__ __forceinline__ void select_final_row(const float* __restrict__ logit
         return;
     }
     if (mode == SEL_SAMPLE && P.beam > 1) return;  // beam rows: beam_topk / beam_update
-    const SelPart r = combine_parts(parts + b * SEL_SPLIT);
+    const SelPart r = combine_parts<false>(parts);  // this row's slices, staged in LDS
     const float lse_all = r.m_all + __logf(r.s_all);
     if (mode == SEL_SOT) {
         const float* x = logits + (int64_t)b * P.V;
@@ -747,12 +750,22 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ l
                                                      int* __restrict__ arrive, int* __restrict__ ticket, int bump) {
     const int step = *pos_ptr;
     select_partial_body(logits, P, step, supmask, st, parts);
-    if (threadIdx.x != 0) return;
-    __builtin_amdgcn_s_waitcnt(0);  // this slice's part stores are complete at device scope
+    __shared__ int last;
+    __shared__ SelPart rp[SEL_SPLIT];
     const int b = blockIdx.x;
-    if (__hip_atomic_fetch_add(ticket + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != SEL_SPLIT - 1) return;
-    __hip_atomic_store(ticket + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-    select_final_row(logits, P, step, prompt, parts, st, cur_tok, tokens, max_tokens);
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_s_waitcnt(0);  // this slice's part stores are complete at device scope
+        last = __hip_atomic_fetch_add(ticket + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == SEL_SPLIT - 1;
+        if (last) __hip_atomic_store(ticket + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+    }
+    __syncthreads();
+    if (!last) return;
+    // one lane per slice fetches it (device scope: written by other workgroups, maybe
+    // on other XCDs); thread 0 combines them in fixed order
+    if (threadIdx.x < SEL_SPLIT) rp[threadIdx.x] = load_part(parts + b * SEL_SPLIT + threadIdx.x);
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    select_final_row(logits, P, step, prompt, rp, st, cur_tok, tokens, max_tokens);
     if (!bump) return;
     __builtin_amdgcn_s_waitcnt(0);
     if (__hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
@@ -818,7 +831,7 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(const float* __restrict_
         return;
     }
     if (tid == 0) {
-        const SelPart r = combine_parts(parts + (int64_t)row * SEL_SPLIT);
+        const SelPart r = combine_parts<false>(parts + (int64_t)row * SEL_SPLIT);
         const float lse_all = r.m_all + logf(r.s_all);
         const float lse_ts = r.m_ts == -INFINITY ? -INFINITY : r.m_ts + logf(r.s_ts);
         stat[0] = lse_all;

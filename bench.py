@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--beam5-steps", type=int, default=3,
                     help="also time this many beam-5 steps on the lanes (after the greedy timed region)")
     ap.add_argument("--cpu-decode-steps", type=int, default=8)
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc.json"),
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_v16_pmc.json"),
                     help="per-kernel HBM bytes from a rocprofv3 --pmc pass (tools/pmc_summary.py)")
     return ap.parse_args()
 

@@ -122,6 +122,39 @@ def test_tiny_greedy_matches_fp16_oracle(tiny_engine):
     assert out.language == r.language
 
 
+def test_wide_batch_greedy_matches_fp16_oracle():
+    """>= 24 decoder rows take the 3-slot ring logits GEMM (gemm_wide_kernel) instead of
+    the skinny one: 32 windows (two clips alternating) against the fp16 oracle, and every
+    copy of a clip decodes identically."""
+    from oracle import decode as odec
+    from oracle.model import WhisperOracle
+    d = D.TINY_TEST
+    w = weights.random_weights(d, seed=1234, emb_std=0.5)
+    eng = WhisperEngine(d, device=0, max_batch=32)
+    try:
+        eng.load_weights(w)
+        st = D.SpecialTokens.for_vocab(d.n_vocab)
+        pcms = [synth.chirp_clip(11, 30.0), synth.chirp_clip(12, 30.0)]
+        n = 32
+        eng.log_mel([pcms[i % 2] for i in range(n)])
+        eng.encode([(i, 0, 3000) for i in range(n)])
+        sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+        cfg = DecodeConfig(suppress_tokens=sup, max_length=64)
+        outs = eng.decode(n, cfg, dump_steps=4)
+        orc = WhisperOracle(d, w, fp16=True)
+        for k in range(2):
+            enc = eng.encoder_output(k)
+            r = odec.greedy_from_encoder(orc, orc.cross_kv(enc), st,
+                                         opts=odec.DecodeOptions(suppress_tokens=sup, max_length=64), keep_logits=4)
+            for i in range(4):
+                np.testing.assert_allclose(outs[k].logits[i], r.step_logits[i], atol=2e-2, rtol=0)
+            assert outs[k].tokens == r.tokens
+            for j in range(k, n, 2):
+                assert outs[j].tokens == outs[k].tokens
+    finally:
+        eng.close()
+
+
 def test_batch_equals_single(tiny_engine):
     """A window's tokens do not depend on what else is in the batch."""
     d, eng, _ = tiny_engine

@@ -165,6 +165,32 @@ __device__ __forceinline__ void reduce_head(const float* __restrict__ part, int 
     __syncthreads();
 }
 
+// q, k and v of one (row, head) at once: thread t < 192 owns element t % 64 of q / k / v
+// (t / 64) and reproduces reduce_head's summation order exactly (per-wave slab sums
+// s = w, w+4, ... then bias + (((w0 + w1) + w2) + w3)), so the result is bit-identical
+// to three reduce_head calls, in one round trip and one barrier instead of three and six.
+__device__ __forceinline__ void reduce_qkv(const float* __restrict__ part, int ks, int64_t slab, int64_t row, int D,
+                                           int h, const float* __restrict__ bias, h16* q16, h16* kdst, h16* vdst) {
+    const int t = threadIdx.x;
+    if (t < 3 * HD) {
+        const int which = t >> 6, d = t & 63;
+        const int64_t off = row + which * D + h * HD + d;
+        float ws[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            float v = 0.f;
+            int s = w;
+            for (; s + 4 < ks; s += 8) v += part[s * slab + off] + part[(s + 4) * slab + off];
+            if (s < ks) v += part[s * slab + off];
+            ws[w] = v;
+        }
+        float r = bias[which * D + h * HD + d];
+        r += ws[0] + ws[1] + ws[2] + ws[3];
+        h16* dst = which == 0 ? q16 : which == 1 ? kdst : vdst;
+        dst[d] = (h16)r;
+    }
+}
+
 // grid (H, B): q,k,v = Σ split-K partials of the fused qkv projection + bias; k,v
 // appended to the cache at the device-side position; attend over 0..pos.
 __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restrict__ part, int ks,
@@ -173,7 +199,6 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
                                                             int H, int B, int ctx, h16* __restrict__ out,
                                                             const int* __restrict__ anc, int group) {
     __shared__ h16 q16[HD];
-    __shared__ float red4[256];
     int h, b;
     if (anc) {
         // beam rows: the `group` hypotheses of one (window, head) run adjacently on one
@@ -193,9 +218,7 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
     h16* kc = kcache + ((int64_t)b * H + h) * ctx * HD;
     h16* vc = vcache + ((int64_t)b * H + h) * ctx * HD;
     const int64_t slab = (int64_t)B * 3 * D, row = (int64_t)b * 3 * D;
-    reduce_head(part, ks, slab, row + h * HD, bias, h * HD, q16, red4);
-    reduce_head(part, ks, slab, row + D + h * HD, bias, D + h * HD, kc + (int64_t)pos * HD, red4);
-    reduce_head(part, ks, slab, row + 2 * D + h * HD, bias, 2 * D + h * HD, vc + (int64_t)pos * HD, red4);
+    reduce_qkv(part, ks, slab, row, D, h, bias, q16, kc + (int64_t)pos * HD, vc + (int64_t)pos * HD);
     __threadfence_block();
     __syncthreads();
     if (anc)

@@ -47,8 +47,9 @@ __device__ __forceinline__ h16x8 ld8(const h16* p) {
 // Attention of one query row over n_keys rows of K/V ([n][64] fp16, contiguous);
 // K/V loads are nontemporal (the self-K/V caches of a step exceed the MALL): 18.7 -> 17.1 us.
 // 256 threads.  Scores live in LDS (n_keys <= MAXK).  Loads are issued in groups
-// (2 K rows = 16 x 16 B per lane, 8 V pieces per lane) before the FMAs that use
-// them so each lane keeps several HBM requests in flight.
+// (8 K pieces = 256 keys, 8 V pieces = 256 keys per lane) before the FMAs that use
+// them, so a 448-key cache costs two HBM round trips per pass (the former 128-key K
+// tiles and one-piece V tail loop cost up to 4 and 8).
 //
 // GATHER (beam search): key p of this row lives in the cache slot of the row that
 // wrote position p of this hypothesis' history: K + soff[p] * slot_stride, where
@@ -80,15 +81,16 @@ __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ 
 #pragma unroll
     for (int i = 0; i < 8; ++i) q[i] = qs[8 * c8 + i];
     float mx = -INFINITY;
-    for (int base = 0; base < n_keys; base += 128) {
-        h16x8 kv[4];
+    // 256 keys (8 loads per lane) per round trip: at most 2 for 448 keys
+    for (int base = 0; base < n_keys; base += 256) {
+        h16x8 kv[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < 8; ++u) {
             const int key = min(base + u * 32 + w * 8 + kr, n_keys - 1);
             kv[u] = ld8<NT>(krow(K, key) + 8 * c8);
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < 8; ++u) {
             float d = 0.f;
 #pragma unroll
             for (int i = 0; i < 8; ++i) d = fmaf((float)kv[u][i], q[i], d);
@@ -114,24 +116,19 @@ __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ 
     // one wave-instruction reads 8 consecutive V rows = 1 KiB contiguous
     const int kg = tid >> 3, c = tid & 7;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    int j = kg;
-    for (; j + 32 * 7 < n_keys; j += 32 * 8) {
+    // 8 V pieces per lane per round trip (keys past the end: clamped address, p = 0, so
+    // the lane's keys are still accumulated in increasing order with nothing added)
+    for (int j = kg; j < n_keys; j += 32 * 8) {
         h16x8 v[8];
         float p[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = ld8<NT>(krow(V, j + 32 * u) + 8 * c);
+        for (int u = 0; u < 8; ++u) v[u] = ld8<NT>(krow(V, min(j + 32 * u, n_keys - 1)) + 8 * c);
 #pragma unroll
-        for (int u = 0; u < 8; ++u) p[u] = sc[j + 32 * u];
+        for (int u = 0; u < 8; ++u) p[u] = j + 32 * u < n_keys ? sc[j + 32 * u] : 0.f;
 #pragma unroll
         for (int u = 0; u < 8; ++u)
 #pragma unroll
             for (int e = 0; e < 8; ++e) acc[e] = fmaf(p[u], (float)v[u][e], acc[e]);
-    }
-    for (; j < n_keys; j += 32) {
-        const h16x8 v = ld8<NT>(krow(V, j) + 8 * c);
-        const float p = sc[j];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] = fmaf(p, (float)v[e], acc[e]);
     }
     part[kg][2 * c] = f32x4{acc[0], acc[1], acc[2], acc[3]};
     part[kg][2 * c + 1] = f32x4{acc[4], acc[5], acc[6], acc[7]};

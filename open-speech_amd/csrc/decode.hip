@@ -919,7 +919,7 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(const float* __restrict_
 
 // grid windows, 256 threads: merge the candidates, register finished hypotheses,
 // pick the surviving beams and reorder their tokens / ancestry / state.
-__global__ __launch_bounds__(256) void beam_update_kernel(SelParams P, const int* __restrict__ pos_ptr,
+__device__ __forceinline__ void beam_update_body(const SelParams& P, const int* __restrict__ pos_ptr,
                                                           SelState* __restrict__ st,
                                                           const BeamCand* __restrict__ cand, int* __restrict__ seq,
                                                           int* __restrict__ anc, int ctx, BeamWin* __restrict__ bwin,
@@ -1046,6 +1046,26 @@ __global__ __launch_bounds__(256) void beam_update_kernel(SelParams P, const int
     }
 }
 
+// grid windows: the per-window merge / finish / reorder, then an arrival count over
+// the windows; the last one advances the device step counter (every window read it
+// at its start), so beam steps need no separate bump launch.
+__global__ __launch_bounds__(256) void beam_update_kernel(SelParams P, int* __restrict__ pos_ptr,
+                                                          SelState* __restrict__ st,
+                                                          const BeamCand* __restrict__ cand, int* __restrict__ seq,
+                                                          int* __restrict__ anc, int ctx, BeamWin* __restrict__ bwin,
+                                                          int* __restrict__ best_tok, int* __restrict__ cur_tok,
+                                                          int max_tokens, int* __restrict__ arrive) {
+    const int step = *pos_ptr;
+    beam_update_body(P, pos_ptr, st, cand, seq, anc, ctx, bwin, best_tok, cur_tok, max_tokens);
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    __builtin_amdgcn_s_waitcnt(0);
+    if (__hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
+        __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(pos_ptr, step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 __global__ void count_done_kernel(const SelState* st, int B, int* out) {
     int c = 0;
     for (int i = threadIdx.x; i < B; i += blockDim.x) c += st[i].done;
@@ -1053,7 +1073,6 @@ __global__ void count_done_kernel(const SelState* st, int B, int* out) {
     if (threadIdx.x == 0) *out = c;
 }
 
-__global__ void bump_kernel(int* p) { *p += 1; }
 }  // namespace
 
 int sel_parts_bytes() { return (int)sizeof(SelPart) * SEL_SPLIT; }
@@ -1103,19 +1122,18 @@ void launch_select(const float* logits, int rows, int* pos, const SelParams& P, 
                                                         cur_tok, tokens, max_tokens, arrive, arrive + 1, bump ? 1 : 0);
 }
 
-void launch_beam(const float* logits, int windows, const int* pos, const SelParams& P, const unsigned* supmask,
+void launch_beam(const float* logits, int windows, int* pos, const SelParams& P, const unsigned* supmask,
                  SelState* st, const void* sel_parts, void* cand, int* seq, int* anc, int ctx, BeamWin* bw,
-                 int* best_tok, int* cur_tok, int max_tokens, hipStream_t s) {
+                 int* best_tok, int* cur_tok, int max_tokens, int* arrive, hipStream_t s) {
     beam_topk_kernel<<<dim3(windows * P.beam, BEAM_SLICES), 256, 0, s>>>(logits, P, pos, supmask, st,
                                                                        (const SelPart*)sel_parts, (BeamCand*)cand);
     beam_update_kernel<<<windows, 256, 0, s>>>(P, pos, st, (const BeamCand*)cand, seq, anc, ctx, bw, best_tok,
-                                                cur_tok, max_tokens);
+                                                cur_tok, max_tokens, arrive);
 }
 
 void launch_count_done(const SelState* st, int rows, int* out, hipStream_t s) {
     count_done_kernel<<<1, 64, 0, s>>>(st, rows, out);
 }
 
-void launch_bump(int* p, hipStream_t s) { bump_kernel<<<1, 1, 0, s>>>(p); }
 
 }  // namespace osw

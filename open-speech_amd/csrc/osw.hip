@@ -40,7 +40,6 @@ void launch_dec_cross_attn(const float*, int, const float*, const h16*, const h1
 void launch_dec_resid_ln(const float*, int, int, int, const float*, float*, const float*, const float*, h16*,
                          const h16*, const float*, const int*, const int*, int, hipStream_t);
 void launch_dec_reduce_gelu(const float*, int, int, int, const float*, h16*, hipStream_t);
-void launch_bump(int*, hipStream_t);
 }  // namespace osw
 
 using namespace osw;
@@ -683,12 +682,11 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
                       c->selp, c->sel_arrive, beam == 1, c->stream);
         if (beam > 1)
             launch_beam(c->logits, nb, c->pos, SP, c->supmask, c->sel, c->selp, c->bcand, c->tokens, c->anc,
-                        d.n_text_ctx, c->bwin, c->btok, c->cur_tok, max_tok, c->stream);
+                        d.n_text_ctx, c->bwin, c->btok, c->cur_tok, max_tok, c->sel_arrive, c->stream);
     };
     auto one_step = [&] {
         decoder_step(c, rows, group, beam > 1);
-        select();  // greedy: select_final advances the step counter itself
-        if (beam > 1) launch_bump(c->pos, c->stream);
+        select();  // the select kernel (greedy) or the beam update advances the step counter
     };
     const int CH = 8;
     const bool graph = c->use_graph && !r->logits_dump && !c->prof_eager;
@@ -744,7 +742,6 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
                                               c->logits + (size_t)b * V, (size_t)V * 4, hipMemcpyDeviceToHost,
                                               c->stream));
                     select();
-                    if (beam > 1) launch_bump(c->pos, c->stream);
                 } else {
                     one_step();
                 }

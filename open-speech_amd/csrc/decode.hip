@@ -323,14 +323,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
     for (int k = 0; k < NB; ++k) {
         mx[k] = -INFINITY;
         if (k >= beam) continue;
+        // beam rows (VALU-bound, §5.5): q in fp16 (exact: fp16(q)/8) and 4 v_dot2_f32_f16
+        // per score instead of 8 conversions + 8 FMAs
         float q[8];
+        h16x2 q2[4];
 #pragma unroll
         for (int i = 0; i < 8; ++i) q[i] = qsh[k][8 * c + i];
 #pragma unroll
+        for (int i = 0; i < 4; ++i) q2[i] = h16x2{(h16)q[2 * i], (h16)q[2 * i + 1]};
+#pragma unroll
         for (int u = 0; u < XU; ++u) {
             float d = 0.f;
+            if constexpr (NB > 1) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) d = fmaf((float)kf[u][i], q[i], d);
+                for (int i = 0; i < 4; ++i)
+                    d = __builtin_amdgcn_fdot2(h16x2{kf[u][2 * i], kf[u][2 * i + 1]}, q2[i], d, false);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) d = fmaf((float)kf[u][i], q[i], d);
+            }
             d += xor_lane<1>(d);
             d += xor_lane<2>(d);
             d += xor_lane<4>(d);

@@ -274,6 +274,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
                                                               int H, int W, int T, int beam, float* __restrict__ ws,
                                                               int* __restrict__ ticket, h16* __restrict__ out) {
     __shared__ float red[4][NB][HD];
+    __shared__ __attribute__((aligned(16))) float pvs[NB > 1 ? 4 : 1][8][HD];  // beam rows' P·V reduction image
     __shared__ float rm[4][NB], rl[4][NB];
     __shared__ float qsh[NB][HD];
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, kg = tid >> 3, c = tid & 7;
@@ -369,22 +370,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
 #pragma unroll
             for (int e = 0; e < 8; ++e) acc[k][e] = fmaf(pu, (float)vf[u][e], acc[k][e]);
         }
-        // the 8 key groups of this wave: lanes c + 8 kr, kr = 0..7
+        // the 8 key groups of this wave: lanes c + 8 kr, kr = 0..7, summed in the order
+        // ((0+1)+(2+3))+((4+5)+(6+7)).  Beam rows (VALU-bound) go through a per-wave LDS
+        // image (2 stores + 8 loads per lane) instead of 24 shuffle-adds per row.
+        if constexpr (NB > 1) {
+            float* t = &pvs[wv][lane >> 3][8 * c];
+            *(f32x4*)t = f32x4{acc[k][0], acc[k][1], acc[k][2], acc[k][3]};
+            *(f32x4*)(t + 4) = f32x4{acc[k][4], acc[k][5], acc[k][6], acc[k][7]};
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            float tv[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            float a = acc[k][e];
-            a += xor_lane<8>(a);
-            a += xor_lane<16>(a);
-            a += xor_lane<32>(a);
-            acc[k][e] = a;
+            for (int r = 0; r < 8; ++r) tv[r] = pvs[wv][r][lane];
+            red[wv][k][lane] = ((tv[0] + tv[1]) + (tv[2] + tv[3])) + ((tv[4] + tv[5]) + (tv[6] + tv[7]));
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                float a = acc[k][e];
+                a += xor_lane<8>(a);
+                a += xor_lane<16>(a);
+                a += xor_lane<32>(a);
+                acc[k][e] = a;
+            }
+            if (lane < 8) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) red[wv][k][8 * c + e] = acc[k][e];
+            }
         }
         float l = c == 0 ? ls[k] : 0.f;
         l = wave_sum(l);
         if (lane == 0) rl[wv][k] = l;
-        if (lane < 8) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) red[wv][k][8 * c + e] = acc[k][e];
-        }
     }
     __syncthreads();
     __shared__ int last;

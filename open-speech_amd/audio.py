@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import io
 import shutil
+import struct
 import subprocess
 import wave
 from math import gcd
@@ -67,3 +68,11 @@ def decode_audio_bytes(data: bytes) -> np.ndarray:
     if p.returncode != 0:
         raise ValueError("ffmpeg could not decode the audio: " + p.stderr.decode(errors="replace")[-300:])
     return np.frombuffer(p.stdout, dtype="<i2").copy()
+
+
+def pcm_to_wav(pcm: bytes, sample_rate: int) -> bytes:
+    """RIFF header + PCM16 mono, byte-identical to ``StreamingSession._pcm_to_wav``
+    (``src/streaming.py:494-516``; pinned by tests/test_ref_fixtures_cpu.py)."""
+    n = len(pcm)
+    return struct.pack("<4sI4s4sIHHIIHH4sI", b"RIFF", 36 + n, b"WAVE", b"fmt ", 16, 1, 1, sample_rate,
+                       sample_rate * 2, 2, 16, b"data", n) + pcm

@@ -19,6 +19,12 @@
  *       loop needs it (FeatureExtractor -> encode -> generate per 30 s window)
  *   osw_get_mel / osw_get_encoder_output / osw_encoder_layer_debug
  *       stage-level read-back used only by the parity tests
+ *   osw_ingest_mean_square + osw_ingest_apply_gain
+ *       replace   preprocess_stt_audio / normalize_gain (src/audio/preprocessing.py:35-63),
+ *                 called at src/main.py:296-300; bit-identical output bytes
+ *   osw_ingest_resample
+ *       replaces  resample_pcm16 (src/streaming.py:55-91; scipy resample_poly,
+ *                 padtype "line"), called at src/streaming.py:293-294; bit-identical
  *
  * Conventions: every call returns 0 (OSW_OK) or a negative code; the message of
  * the last failure on the calling thread is osw_last_error().  Host buffers are
@@ -173,6 +179,26 @@ int osw_set_profiling(osw_ctx* ctx, int32_t enable);
 int osw_get_profile(osw_ctx* ctx, osw_profile* out);
 /* Device stream used by the context (hipStream_t as void*). */
 void* osw_stream(osw_ctx* ctx);
+
+/* ---- audio ingest (context-free: a per-device stream and scratch inside the library).
+ * Host buffers in and out; the arithmetic runs on `device` and is bit-identical to the
+ * reference's numpy / scipy code (csrc/ingest.hip).
+ *
+ * *out_mean = np.mean(np.square(mono)) in float32 with numpy's reduction order, where
+ * mono = channel mean of pcm / 32768 (wav_bytes_to_float32_mono, preprocessing.py:9-20).
+ * The caller derives the gain from it exactly as normalize_gain does (sqrt, log10,
+ * 10 ** (dB / 20) on float32 scalars: preprocessing.py:36-41) and then calls
+ * osw_ingest_apply_gain (apply_gain = 0 when normalize_gain returns early). */
+int osw_ingest_mean_square(int32_t device, const int16_t* pcm, int64_t n_frames, int32_t channels, float* out_mean);
+/* out[n_frames] = int16(clip(clip(mono * gain, -1, 1), -1, 1) * 32767) (truncating) */
+int osw_ingest_apply_gain(int32_t device, const int16_t* pcm, int64_t n_frames, int32_t channels, int32_t apply_gain,
+                          float gain, int16_t* out);
+/* out[n_out] = resample_poly(pcm, up, down, padtype="line") clipped and truncated to
+ * int16; h = the float32 filter resample_poly designs (firwin(2*10*max(up,down)+1,
+ * 1/max(up,down), kaiser 5.0) cast to float32, times up), n_h odd; up/down already
+ * divided by their gcd; n_in >= 2; n_out = ceil(n_in * up / down). */
+int osw_ingest_resample(int32_t device, const int16_t* pcm, int64_t n_in, int32_t up, int32_t down, const float* h,
+                        int32_t n_h, int16_t* out, int64_t n_out);
 
 #ifdef __cplusplus
 }

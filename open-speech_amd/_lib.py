@@ -83,6 +83,11 @@ _SIGS = {
     "osw_set_profiling": (C.c_int, [C.c_void_p, C.c_int32]),
     "osw_get_profile": (C.c_int, [C.c_void_p, P(osw_profile)]),
     "osw_stream": (C.c_void_p, [C.c_void_p]),
+    "osw_ingest_mean_square": (C.c_int, [C.c_int32, P(C.c_int16), C.c_int64, C.c_int32, P(C.c_float)]),
+    "osw_ingest_apply_gain": (C.c_int, [C.c_int32, P(C.c_int16), C.c_int64, C.c_int32, C.c_int32, C.c_float,
+                                        P(C.c_int16)]),
+    "osw_ingest_resample": (C.c_int, [C.c_int32, P(C.c_int16), C.c_int64, C.c_int32, C.c_int32, P(C.c_float),
+                                      C.c_int32, P(C.c_int16), C.c_int64]),
 }
 EXPORTED = tuple(_SIGS)
 
@@ -108,7 +113,23 @@ def load() -> C.CDLL:
         return lib
 
 
+OSW_EHIP = -100
+
+
+class OswError(RuntimeError):
+    """A non-zero return code of libosw_hip.so (``rc``) with its osw_last_error() text."""
+
+    def __init__(self, msg: str, rc: int):
+        super().__init__(msg)
+        self.rc = rc
+
+
+class OswDeviceError(OswError):
+    """OSW_EHIP: a HIP runtime error on the context's device (the batcher fails the GPU over)."""
+
+
 def check(rc: int, what: str = "") -> None:
     if rc != OSW_OK:
         msg = load().osw_last_error().decode(errors="replace")
-        raise RuntimeError(f"{what} failed ({rc}): {msg}")
+        cls = OswDeviceError if rc == OSW_EHIP else OswError
+        raise cls(f"{what} failed ({rc}): {msg}", rc)

@@ -173,17 +173,30 @@ class HipWhisperBackend:
         return Path(model_store.cache_dirs(self._settings.get("stt_model_dir", None))[0])
 
     def list_cached_models(self) -> list[dict[str, Any]]:
+        """``FasterWhisperBackend.list_cached_models`` (src/backends/faster_whisper.py:103-172):
+        with ``STT_MODEL_DIR`` set, every non-hidden directory counts (``models--Org--Name``
+        as ``Org/Name``, anything else under its own name); in the HF cache only
+        ``models--Org--Name``."""
         root = self._cache_root()
+        custom = bool(self._settings.get("stt_model_dir", None))
         out, seen = [], set()
         default_model = self._settings.get("stt_default_model", None)
         if root.exists():
             for p in root.iterdir():
-                if not p.is_dir() or not p.name.startswith("models--"):
+                if not p.is_dir() or (custom and p.name.startswith(".")):
                     continue
-                parts = p.name.split("--", 2)
-                if len(parts) != 3:
+                if p.name.startswith("models--"):
+                    parts = p.name.split("--", 2)
+                    if len(parts) != 3:
+                        if not custom:
+                            continue
+                        mid = p.name
+                    else:
+                        mid = f"{parts[1]}/{parts[2]}"
+                elif custom:
+                    mid = p.name
+                else:
                     continue
-                mid = f"{parts[1]}/{parts[2]}"
                 seen.add(mid)
                 size = sum(f.stat().st_size for f in p.rglob("*") if f.is_file()) / (1024 * 1024)
                 out.append({"model": mid, "loaded": mid in self._models, "is_default": mid == default_model,
@@ -194,8 +207,19 @@ class HipWhisperBackend:
         return out
 
     def _find_cache_path(self, model_id: str) -> Path | None:
-        p = self._cache_root() / ("models--" + model_id.replace("/", "--"))
-        return p if p.exists() else None
+        """``_find_cache_path`` (src/backends/faster_whisper.py:174-195): ``models--Org--Name``,
+        and with ``STT_MODEL_DIR`` set also ``<dir>/<Name>``."""
+        root = self._cache_root()
+        if not root.exists():
+            return None
+        p = root / ("models--" + model_id.replace("/", "--"))
+        if p.exists():
+            return p
+        if self._settings.get("stt_model_dir", None):
+            p = root / model_id.split("/")[-1]
+            if p.exists():
+                return p
+        return None
 
     def delete_cached_model(self, model_id: str) -> bool:
         p = self._find_cache_path(model_id)

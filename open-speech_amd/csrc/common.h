@@ -115,7 +115,20 @@ struct GemmArgs {
     int heads_T, heads_H, heads_nb;      // EPI_HEADS geometry
     int band;                            // 256-tile walk: column band width (0 = all columns)
     int kc;                              // 128-tile split-K: K per blockIdx.z, EPI_F32 slab z at C + z*M*ldc (0 = K)
+    // decoder activations as an fp16 pair a = hi + lo (hi = fp16(a), lo = fp16(a - hi)):
+    // A_lo has A's row addressing; the kernels accumulate hi·W then lo·W into the same
+    // fp32 accumulators, so the product carries ~22 bits of the fp32 activation.
+    // nullptr: A alone (fp16 activations).  Supported by the skinny, wide and 128-tile
+    // kernels (the decoder's); the encoder's 256-tile kernels ignore it (host-checked).
+    const h16* A_lo;
 };
+
+// fp32 -> (hi, lo) fp16 pair: hi = fp16(v), lo = fp16(v - hi)
+__device__ __forceinline__ void split_h16(float v, h16* hi, h16* lo, int64_t i) {
+    const h16 h = (h16)v;
+    hi[i] = h;
+    lo[i] = (h16)(v - (float)h);
+}
 
 // launchers (defined in the .hip files)
 void launch_gemm(const GemmArgs& g, hipStream_t s);

@@ -56,8 +56,8 @@ __device__ __forceinline__ h16x8 ld8(const h16* p) {
 // soff[p] = anc[p] - self (staged in LDS; the newest key is always this row's own).
 template <int MAXK, bool GATHER = false, bool NT = !GATHER>
 __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ K, const h16* __restrict__ V,
-                           int n_keys, h16* __restrict__ out, const int* __restrict__ anc = nullptr, int self = 0,
-                           int64_t slot_stride = 0) {
+                           int n_keys, h16* __restrict__ out, int64_t lo_off, const int* __restrict__ anc = nullptr,
+                           int self = 0, int64_t slot_stride = 0) {
     __shared__ float qs[HD];
     __shared__ float sc[MAXK];
     __shared__ float red[8];
@@ -137,7 +137,7 @@ __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ 
         const int cc = tid >> 3, e = tid & 7;
         float r = 0.f;
         for (int k = 0; k < 32; ++k) r += part[k][2 * cc + (e >> 2)][e & 3];
-        out[tid] = (h16)(r / sum);
+        split_h16(r / sum, out, out + lo_off, tid);  // hi/lo pair: the o-projection's operand
     }
 }
 
@@ -194,7 +194,7 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
                                                             const float* __restrict__ bias, h16* __restrict__ kcache,
                                                             h16* __restrict__ vcache, const int* __restrict__ pos_ptr,
                                                             int H, int B, int ctx, h16* __restrict__ out,
-                                                            const int* __restrict__ anc, int group) {
+                                                            int64_t lo_off, const int* __restrict__ anc, int group) {
     __shared__ h16 q16[HD];
     int h, b;
     if (anc) {
@@ -219,10 +219,10 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
     __threadfence_block();
     __syncthreads();
     if (anc)
-        attend_one<448, true>(q16, kc, vc, pos + 1, out + (int64_t)b * D + h * HD, anc + (int64_t)b * ctx, b,
+        attend_one<448, true>(q16, kc, vc, pos + 1, out + (int64_t)b * D + h * HD, lo_off, anc + (int64_t)b * ctx, b,
                               (int64_t)H * ctx * HD);
     else
-        attend_one<448>(q16, kc, vc, pos + 1, out + (int64_t)b * D + h * HD);
+        attend_one<448>(q16, kc, vc, pos + 1, out + (int64_t)b * D + h * HD, lo_off);
 }
 
 // grid H*B (flattened): q = Σ split-K partials of the cross-attention q projection
@@ -232,7 +232,8 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
 __global__ __launch_bounds__(256) void dec_cross_attn_kernel(const float* __restrict__ part, int ks,
                                                              const float* __restrict__ bias,
                                                              const h16* __restrict__ xk, const h16* __restrict__ xv,
-                                                             int H, int B, int T, int beam, h16* __restrict__ out) {
+                                                             int H, int B, int T, int beam, h16* __restrict__ out,
+                                                             int64_t lo_off) {
     __shared__ h16 q16[HD];
     __shared__ float red4[256];
     const int nwg = gridDim.x, bid = blockIdx.x;
@@ -243,7 +244,7 @@ __global__ __launch_bounds__(256) void dec_cross_attn_kernel(const float* __rest
     const int D = H * HD;
     reduce_head(part, ks, (int64_t)B * D, (int64_t)b * D + h * HD, bias, h * HD, q16, red4);
     const int64_t hoff = ((int64_t)w * H + h) * T * HD;
-    attend_one<1536>(q16, xk + hoff, xv + hoff, T, out + (int64_t)b * D + h * HD);
+    attend_one<1536>(q16, xk + hoff, xv + hoff, T, out + (int64_t)b * D + h * HD, lo_off);
 }
 
 // ---------------------------------------------------------------------------
@@ -272,7 +273,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
                                                               const float* __restrict__ bias,
                                                               const h16* __restrict__ xk, const h16* __restrict__ xv,
                                                               int H, int W, int T, int beam, float* __restrict__ ws,
-                                                              int* __restrict__ ticket, h16* __restrict__ out) {
+                                                              int* __restrict__ ticket, h16* __restrict__ out,
+                                                              int64_t lo_off) {
     __shared__ float red[4][NB][HD];
     __shared__ __attribute__((aligned(16))) float pvs[NB > 1 ? 4 : 1][8][HD];  // beam rows' P·V reduction image
     __shared__ float rm[4][NB], rl[4][NB];
@@ -314,7 +316,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
             if (k >= beam) break;
             float r = bias[h * HD + lane];
             r += red[0][k][lane] + red[1][k][lane] + red[2][k][lane] + red[3][k][lane];
-            qsh[k][lane] = (float)(h16)r * 0.125f;
+            qsh[k][lane] = (float)(h16)r;  // fp16(q); the 1/sqrt(64) scale is applied in fp32 below
         }
     }
     __syncthreads();
@@ -324,14 +326,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
     for (int k = 0; k < NB; ++k) {
         mx[k] = -INFINITY;
         if (k >= beam) continue;
-        // beam rows (VALU-bound, §5.5): q in fp16 (exact: fp16(q)/8) and 4 v_dot2_f32_f16
-        // per score instead of 8 conversions + 8 FMAs
+        // beam rows (VALU-bound, §5.5): 4 v_dot2_f32_f16 per score on the unscaled fp16 q
+        // (exact: qsh holds fp16 values) instead of 8 conversions + 8 FMAs, then the
+        // 1/sqrt(64) scale in fp32 (exact, a power of two); one row: q * 0.125 in fp32
         float q[8];
         h16x2 q2[4];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) q[i] = qsh[k][8 * c + i];
+        for (int i = 0; i < 8; ++i) q[i] = qsh[k][8 * c + i] * 0.125f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) q2[i] = h16x2{(h16)q[2 * i], (h16)q[2 * i + 1]};
+        for (int i = 0; i < 4; ++i) q2[i] = h16x2{(h16)qsh[k][8 * c + 2 * i], (h16)qsh[k][8 * c + 2 * i + 1]};
 #pragma unroll
         for (int u = 0; u < XU; ++u) {
             float d = 0.f;
@@ -339,6 +342,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
                     d = __builtin_amdgcn_fdot2(h16x2{kf[u][2 * i], kf[u][2 * i + 1]}, q2[i], d, false);
+                d *= 0.125f;
             } else {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) d = fmaf((float)kf[u][i], q[i], d);
@@ -453,7 +457,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
             L = fmaf(__hip_atomic_load(src + q * XPART + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), e, L);
             O = fmaf(__hip_atomic_load(src + q * XPART + 4 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), e, O);
         }
-        out[(int64_t)(r0 + k) * D + h * HD + lane] = (h16)(O / L);
+        split_h16(O / L, out, out + lo_off, (int64_t)(r0 + k) * D + h * HD + lane);
     }
 }
 
@@ -464,7 +468,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
 __global__ __launch_bounds__(1024) void dec_resid_ln_kernel(const float* __restrict__ part, int ks, int B, int D,
                                                             const float* __restrict__ bias, float* __restrict__ x,
                                                             const float* __restrict__ g, const float* __restrict__ be,
-                                                            h16* __restrict__ y, const h16* __restrict__ tok_emb,
+                                                            h16* __restrict__ y, int64_t lo_off,
+                                                            const h16* __restrict__ tok_emb,
                                                             const float* __restrict__ pos_emb,
                                                             const int* __restrict__ tok,
                                                             const int* __restrict__ pos_ptr, int ctx) {
@@ -514,18 +519,18 @@ __global__ __launch_bounds__(1024) void dec_resid_ln_kernel(const float* __restr
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
         const int c = tid + 1024 * i;
-        if (c < D) y[rb + c] = (h16)((v[i] - mean) * rstd * g[c] + be[c]);
+        if (c < D) split_h16((v[i] - mean) * rstd * g[c] + be[c], y, y + lo_off, rb + c);
     }
 }
 
 // fc1: h[b][n] = fp16(gelu(bias + Σ partials))
 __global__ __launch_bounds__(256) void dec_reduce_gelu_kernel(const float* __restrict__ part, int ks, int64_t total,
                                                               int N, const float* __restrict__ bias,
-                                                              h16* __restrict__ y) {
+                                                              h16* __restrict__ y, int64_t lo_off) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
         float v = bias[i % N];
         for (int k = 0; k < ks; ++k) v += part[k * total + i];
-        y[i] = (h16)gelu_erf(v);
+        split_h16(gelu_erf(v), y, y + lo_off, i);
     }
 }
 
@@ -1109,39 +1114,41 @@ int sel_parts_bytes() { return (int)sizeof(SelPart) * SEL_SPLIT; }
 int beam_cand_bytes(int beam) { return (int)sizeof(BeamCand) * BEAM_SLICES * 2 * beam; }
 
 void launch_dec_self_attn(const float* part, int ks, const float* bias, h16* kc, h16* vc, const int* pos, int B,
-                          int H, int ctx, h16* out, const int* anc, int group, hipStream_t s) {
-    dec_self_attn_kernel<<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, anc, anc ? group : 1);
+                          int H, int ctx, h16* out, int64_t lo_off, const int* anc, int group, hipStream_t s) {
+    dec_self_attn_kernel<<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, lo_off, anc,
+                                               anc ? group : 1);
 }
 
 void launch_dec_cross_attn(const float* part, int ks, const float* bias, const h16* xk, const h16* xv, int B, int H,
-                           int T, int beam, h16* out, float* ws, int* ticket, hipStream_t s) {
+                           int T, int beam, h16* out, int64_t lo_off, float* ws, int* ticket, hipStream_t s) {
     static const bool legacy = std::getenv("OSW_XATTN_LEGACY") != nullptr;  // A/B switch: one workgroup per (row, head)
     if (legacy || !ws) {
-        dec_cross_attn_kernel<<<H * B, 256, 0, s>>>(part, ks, bias, xk, xv, H, B, T, beam, out);
+        dec_cross_attn_kernel<<<H * B, 256, 0, s>>>(part, ks, bias, xk, xv, H, B, T, beam, out, lo_off);
         return;
     }
     const int W = B / beam;
     const unsigned grid = (unsigned)(((W * H + 7) / 8) * 8 * XCH);
     switch (beam) {
-        case 1: dec_xattn_chunk_kernel<1><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out); break;
-        case 2: dec_xattn_chunk_kernel<2><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out); break;
+        case 1: dec_xattn_chunk_kernel<1><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off); break;
+        case 2: dec_xattn_chunk_kernel<2><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off); break;
         case 3:
-        case 4: dec_xattn_chunk_kernel<4><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out); break;
-        case 5: dec_xattn_chunk_kernel<5><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out); break;
-        default: dec_xattn_chunk_kernel<8><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out); break;
+        case 4: dec_xattn_chunk_kernel<4><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off); break;
+        case 5: dec_xattn_chunk_kernel<5><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off); break;
+        default: dec_xattn_chunk_kernel<8><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off); break;
     }
 }
 
 void launch_dec_resid_ln(const float* part, int ks, int B, int D, const float* bias, float* x, const float* g,
-                         const float* be, h16* y, const h16* tok_emb, const float* pos_emb, const int* tok,
-                         const int* pos, int ctx, hipStream_t s) {
-    dec_resid_ln_kernel<<<B, 1024, 0, s>>>(part, ks, B, D, bias, x, g, be, y, tok_emb, pos_emb, tok, pos, ctx);
+                         const float* be, h16* y, int64_t lo_off, const h16* tok_emb, const float* pos_emb,
+                         const int* tok, const int* pos, int ctx, hipStream_t s) {
+    dec_resid_ln_kernel<<<B, 1024, 0, s>>>(part, ks, B, D, bias, x, g, be, y, lo_off, tok_emb, pos_emb, tok, pos, ctx);
 }
 
-void launch_dec_reduce_gelu(const float* part, int ks, int B, int N, const float* bias, h16* y, hipStream_t s) {
+void launch_dec_reduce_gelu(const float* part, int ks, int B, int N, const float* bias, h16* y, int64_t lo_off,
+                            hipStream_t s) {
     const int64_t total = (int64_t)B * N;
     dec_reduce_gelu_kernel<<<(unsigned)std::min<int64_t>((total + 255) / 256, 1024), 256, 0, s>>>(part, ks, total, N,
-                                                                                                 bias, y);
+                                                                                                 bias, y, lo_off);
 }
 
 void launch_select(const float* logits, int rows, int* pos, const SelParams& P, const int* prompt,

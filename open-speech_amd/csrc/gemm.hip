@@ -56,15 +56,19 @@ __device__ __forceinline__ void store_one(const GemmArgs& g, int m, int n, float
     }
 }
 
-template <int EPI>
-__global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
-    __shared__ __attribute__((aligned(16))) h16 lds[2][2][BM * BK];  // [buf][A|W], 64 KiB
+// LO (hi/lo activations, GemmArgs::A_lo; decoder beam rows > 64): a third LDS
+// image per stage and two MFMAs per fragment pair; 96 KiB -> one workgroup per CU.
+template <int EPI, bool LO = false>
+__global__ __launch_bounds__(NTHR, LO ? 1 : 2) void gemm_kernel(GemmArgs g) {
+    constexpr int NIMG = LO ? 3 : 2;  // [A | W | A_lo]
+    __shared__ __attribute__((aligned(16))) h16 lds[2][NIMG][BM * BK];  // [buf][A|W(|A_lo)], 64 / 96 KiB
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
     const int kc = g.kc > 0 ? g.kc : g.K, kbeg = blockIdx.z * kc;  // split-K: slab blockIdx.z
 
     // per-thread source rows for the 4 A and 4 W glds pieces (fixed over K)
     const h16* asrc[4];
+    const h16* lsrc[LO ? 4 : 1];
     const h16* wsrc[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -73,6 +77,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
         const int gm = min(m0 + r, g.M - 1);
         const int gn = min(n0 + r, g.N - 1);
         asrc[i] = grp_row(g.A, gm, g.a_grp_rows, g.a_grp_stride, g.lda) + c * 8 + kbeg;
+        if constexpr (LO) lsrc[i] = grp_row(g.A_lo, gm, g.a_grp_rows, g.a_grp_stride, g.lda) + c * 8 + kbeg;
         wsrc[i] = g.W + (int64_t)gn * g.ldw + c * 8 + kbeg;
     }
 
@@ -83,6 +88,9 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
             h16* dw = &lds[buf][1][(i * 4 + wave) * 8 * BK];
             __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + k0), (OSW_LDS void*)da, 16, 0, 0);
             __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + k0), (OSW_LDS void*)dw, 16, 0, 0);
+            if constexpr (LO)
+                __builtin_amdgcn_global_load_lds((const void*)(lsrc[i] + k0),
+                                                 (OSW_LDS void*)&lds[buf][NIMG - 1][(i * 4 + wave) * 8 * BK], 16, 0, 0);
         }
     };
 
@@ -102,14 +110,16 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
         if (kt + 1 < nk) stage(buf ^ 1, (kt + 1) * BK);
         const h16* la = lds[buf][0];
         const h16* lw = lds[buf][1];
+        const h16* ll = lds[buf][NIMG - 1];
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             const int c = ks * 4 + (lane >> 4);
-            h16x8 a[4], b[4];
+            h16x8 a[4], b[4], al[LO ? 4 : 1];
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi) {
                 const int row = wm * 64 + mi * 16 + (lane & 15);
                 a[mi] = *(const h16x8*)&la[row * BK + swz(row, c) * 8];
+                if constexpr (LO) al[mi] = *(const h16x8*)&ll[row * BK + swz(row, c) * 8];
             }
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni) {
@@ -119,8 +129,11 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-                for (int ni = 0; ni < 4; ++ni)
+                for (int ni = 0; ni < 4; ++ni) {
                     acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+                    if constexpr (LO)
+                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[mi], b[ni], acc[mi][ni], 0, 0, 0);
+                }
         }
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
@@ -567,20 +580,27 @@ __device__ __forceinline__ void wait_vmcnt() {
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <int MT, bool DIRECT, int EPI>
+template <int MT, bool DIRECT, int EPI, bool LO>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, float* __restrict__ part) {
     // Workgroup = 64 columns x one kc-deep K range; wave = 16 columns.  The
-    // activation rows (M <= 64) of each 256-deep K chunk are staged ONCE per
+    // activation rows (M <= 64) of each CKK-deep K chunk are staged ONCE per
     // workgroup into LDS by global_load_lds (row-XOR swizzle on the 16-B chunk ->
     // conflict-free ds_read_b128), instead of every wave re-reading them from L2
-    // (4x the weight bytes at M = 64).  Weights stream straight to VGPRs, 8 x 16 B
+    // (4x the weight bytes at M = 64).  Weights stream straight to VGPRs, CK x 16 B
     // per lane per chunk, the next chunk's loads issued before the current chunk's
     // MFMAs (two register sets, manual 2x unroll).  Loads are unconditional (clamped
     // addresses for a short last chunk) so hipcc never branches around them.
-    constexpr int CK = 8;            // k32 steps per chunk (256 k)
+    // LO: a second image holds the activations' lo halves (GemmArgs::A_lo); every
+    // weight fragment feeds two MFMAs (hi, then lo) into one accumulator.  At > 32
+    // rows the chunk is 128 k so both images still fit 64 KB (2 workgroups per CU).
+    constexpr int CK = (LO && MT > 2) ? 4 : 8;  // k32 steps per chunk
+    constexpr int CKK = CK * 32;                 // k per chunk
+    constexpr int CPR = CKK / 8;                 // 16-B pieces of one row per chunk
+    constexpr int RPP = 64 / CPR;                // rows per 1-KiB glds wave-instruction
     constexpr int ROWS = MT * 16;
-    constexpr int APIECES = ROWS / 8;  // 1-KiB glds pieces per wave per chunk (2 rows each, 4 waves)
-    __shared__ __attribute__((aligned(16))) h16 As[2][ROWS * 256];
+    constexpr int NIMG = LO ? 2 : 1;
+    constexpr int APIECES = ROWS / RPP / 4;      // glds per wave per image per chunk
+    __shared__ __attribute__((aligned(16))) h16 As[2][NIMG][ROWS * CKK];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nb = blockIdx.x * 64 + wave * 16;
     const int ks = blockIdx.y;
@@ -591,25 +611,29 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
     const int nsteps = kc / 32;  // multiple of 4
     const int nch = (nsteps + CK - 1) / CK;
 
-    const h16* asrc[APIECES];
+    const h16* asrc[NIMG][APIECES];
     int acl[APIECES];
 #pragma unroll
     for (int i = 0; i < APIECES; ++i) {
         const int j = i * 4 + wave;
-        const int row = 2 * j + (lane >> 5);
-        acl[i] = ((lane & 31) ^ (row & 15)) * 8;
-        asrc[i] = grp_row(g.A, min(mb + row, g.M - 1), g.a_grp_rows, g.a_grp_stride, g.lda) + k0;
+        const int row = RPP * j + lane / CPR;
+        acl[i] = ((lane % CPR) ^ (row & 15)) * 8;
+        const int64_t gr = min(mb + row, g.M - 1);
+        asrc[0][i] = grp_row(g.A, gr, g.a_grp_rows, g.a_grp_stride, g.lda) + k0;
+        if constexpr (LO) asrc[NIMG - 1][i] = grp_row(g.A_lo, gr, g.a_grp_rows, g.a_grp_stride, g.lda) + k0;
     }
     auto stageA = [&](int buf, int c) {
-        // a short last chunk is staged from kc-256 so every load stays inside this K range;
-        // with kc < 256 the unused tail is clamped to the range's last 16 B (values unused)
-        const int kk = min(c * 256, kc - 256 > 0 ? kc - 256 : 0);
+        // a short last chunk is staged from kc-CKK so every load stays inside this K range;
+        // with kc < CKK the unused tail is clamped to the range's last 16 B (values unused)
+        const int kk = min(c * CKK, kc - CKK > 0 ? kc - CKK : 0);
 #pragma unroll
-        for (int i = 0; i < APIECES; ++i) {
-            const int j = i * 4 + wave;
-            __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + min(kk + acl[i], kc - 8)),
-                                             (OSW_LDS void*)&As[buf][2 * j * 256], 16, 0, 0);
-        }
+        for (int im = 0; im < NIMG; ++im)
+#pragma unroll
+            for (int i = 0; i < APIECES; ++i) {
+                const int j = i * 4 + wave;
+                __builtin_amdgcn_global_load_lds((const void*)(asrc[im][i] + min(kk + acl[i], kc - 8)),
+                                                 (OSW_LDS void*)&As[buf][im][RPP * j * CKK], 16, 0, 0);
+            }
     };
     auto loadW = [&](h16x8 (&wf)[CK], int c) {
 #pragma unroll
@@ -624,8 +648,8 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
     const int li = lane & 15, gq = lane >> 4;
     auto consume = [&](const h16x8 (&wf)[CK], int buf, int c) {
         const int steps = min(CK, nsteps - c * CK);
-        // a short last chunk was staged from kc-256: its k32 steps sit at the end of the image
-        const int shift = (c * 256 > kc - 256 && kc >= 256) ? (c * 256 - (kc - 256)) / 32 : 0;
+        // a short last chunk was staged from kc-CKK: its k32 steps sit at the end of the image
+        const int shift = (c * CKK > kc - CKK && kc >= CKK) ? (c * CKK - (kc - CKK)) / 32 : 0;
 #pragma unroll
         for (int u = 0; u < CK; ++u) {
             if (u >= steps) break;
@@ -633,11 +657,16 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
             for (int mt = 0; mt < MT; ++mt) {
                 const int row = mt * 16 + li;
                 const int ch = ((u + shift) * 4 + gq) ^ (row & 15);
-                const h16x8 af = *(const h16x8*)&As[buf][row * 256 + ch * 8];
+                const h16x8 af = *(const h16x8*)&As[buf][0][row * CKK + ch * 8];
                 acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, wf[u], acc[mt], 0, 0, 0);
+                if constexpr (LO) {
+                    const h16x8 al = *(const h16x8*)&As[buf][NIMG - 1][row * CKK + ch * 8];
+                    acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, wf[u], acc[mt], 0, 0, 0);
+                }
             }
         }
     };
+    constexpr int INFLIGHT = CK + NIMG * APIECES;  // one chunk's loads per lane
     h16x8 wa[CK], wb[CK];
     loadW(wa, 0);
     stageA(0, 0);
@@ -645,7 +674,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
         if (c + 1 < nch) {
             loadW(wb, c + 1);
             stageA(1, c + 1);
-            wait_vmcnt<CK + APIECES>();
+            wait_vmcnt<INFLIGHT>();
         } else {
             wait_vmcnt<0>();
         }
@@ -657,7 +686,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
         if (c + 2 < nch) {
             loadW(wa, c + 2);
             stageA(0, c + 2);
-            wait_vmcnt<CK + APIECES>();
+            wait_vmcnt<INFLIGHT>();
         } else {
             wait_vmcnt<0>();
         }
@@ -691,19 +720,24 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
 // per K tile.  fp32 out, written through L2 (device-scope stores) for the select
 // kernels.
 constexpr int WBM = 64, WBN = 128, WSL = 3;
-__global__ __launch_bounds__(256, 2) void gemm_wide_kernel(GemmArgs g) {
-    __shared__ __attribute__((aligned(16))) h16 la[WSL][WBM * BK];
+// LO (hi/lo activations, GemmArgs::A_lo): a second A ring image and two MFMAs per
+// fragment pair; 96 KB of LDS -> one workgroup per CU.
+template <bool LO>
+__global__ __launch_bounds__(256, LO ? 1 : 2) void gemm_wide_kernel(GemmArgs g) {
+    constexpr int NIMG = LO ? 2 : 1;
+    __shared__ __attribute__((aligned(16))) h16 la[WSL][NIMG][WBM * BK];
     __shared__ __attribute__((aligned(16))) h16 lw[WSL][WBN * BK];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n0 = blockIdx.x * WBN;
     // staging: one wave-instruction fills 8 rows x 64 k (1 KiB); A 8 groups (2 per
-    // wave), W 16 groups (4 per wave); the 16-B chunk is XOR-swizzled by row
-    const h16* asrc[2];
+    // wave) per image, W 16 groups (4 per wave); the 16-B chunk is XOR-swizzled by row
+    const h16* asrc[NIMG][2];
     const h16* wsrc[4];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int r = (i * 4 + wave) * 8 + (lane >> 3);
-        asrc[i] = g.A + (int64_t)min(r, g.M - 1) * g.lda + swz(r, lane & 7) * 8;
+        asrc[0][i] = g.A + (int64_t)min(r, g.M - 1) * g.lda + swz(r, lane & 7) * 8;
+        if constexpr (LO) asrc[NIMG - 1][i] = g.A_lo + (int64_t)min(r, g.M - 1) * g.lda + swz(r, lane & 7) * 8;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -712,9 +746,11 @@ __global__ __launch_bounds__(256, 2) void gemm_wide_kernel(GemmArgs g) {
     }
     auto stage = [&](int slot, int k0) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-            __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + k0), (OSW_LDS void*)&la[slot][(i * 4 + wave) * 8 * BK],
-                                             16, 0, 0);
+        for (int im = 0; im < NIMG; ++im)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                __builtin_amdgcn_global_load_lds((const void*)(asrc[im][i] + k0),
+                                                 (OSW_LDS void*)&la[slot][im][(i * 4 + wave) * 8 * BK], 16, 0, 0);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + k0), (OSW_LDS void*)&lw[slot][(i * 4 + wave) * 8 * BK],
@@ -730,22 +766,24 @@ __global__ __launch_bounds__(256, 2) void gemm_wide_kernel(GemmArgs g) {
     if (nk > 1) stage(1, BK);
     for (int kt = 0; kt < nk; ++kt) {
         if (kt + 1 < nk)
-            wait_vmcnt<6>();  // this thread's tile kt has landed; tile kt+1 stays in flight
+            wait_vmcnt<2 * NIMG + 4>();  // this thread's tile kt has landed; tile kt+1 stays in flight
         else
             wait_vmcnt<0>();
         __syncthreads();  // every thread's tile kt has landed; slot (kt+2)%3 is no longer read
         if (kt + 2 < nk) stage((kt + 2) % WSL, (kt + 2) * BK);
-        const h16* A = la[kt % WSL];
-        const h16* W = lw[kt % WSL];
+        const int sl = kt % WSL;
+        const h16* W = lw[sl];
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             const int c = ks * 4 + (lane >> 4);
-            h16x8 a[4], b[2];
+            h16x8 a[NIMG][4], b[2];
 #pragma unroll
-            for (int mi = 0; mi < 4; ++mi) {
-                const int row = mi * 16 + (lane & 15);
-                a[mi] = *(const h16x8*)&A[row * BK + swz(row, c) * 8];
-            }
+            for (int im = 0; im < NIMG; ++im)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi) {
+                    const int row = mi * 16 + (lane & 15);
+                    a[im][mi] = *(const h16x8*)&la[sl][im][row * BK + swz(row, c) * 8];
+                }
 #pragma unroll
             for (int ni = 0; ni < 2; ++ni) {
                 const int row = wave * 32 + ni * 16 + (lane & 15);
@@ -754,8 +792,11 @@ __global__ __launch_bounds__(256, 2) void gemm_wide_kernel(GemmArgs g) {
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-                for (int ni = 0; ni < 2; ++ni)
-                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+                for (int ni = 0; ni < 2; ++ni) {
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0][mi], b[ni], acc[mi][ni], 0, 0, 0);
+                    if constexpr (LO)
+                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[NIMG - 1][mi], b[ni], acc[mi][ni], 0, 0, 0);
+                }
         }
     }
 #pragma unroll
@@ -789,9 +830,11 @@ void skinny_dispatch(const GemmArgs& g, int ksplit, float* part, hipStream_t s) 
     const dim3 grid((g.N + 63) / 64, ksplit);
     const int kc = g.K / ksplit;
     if (ksplit == 1) {
-        gemm_skinny_kernel<MT, true, EPI><<<grid, 256, 0, s>>>(g, kc, part);
+        if (g.A_lo) gemm_skinny_kernel<MT, true, EPI, true><<<grid, 256, 0, s>>>(g, kc, part);
+        else gemm_skinny_kernel<MT, true, EPI, false><<<grid, 256, 0, s>>>(g, kc, part);
     } else {
-        gemm_skinny_kernel<MT, false, EPI><<<grid, 256, 0, s>>>(g, kc, part);
+        if (g.A_lo) gemm_skinny_kernel<MT, false, EPI, true><<<grid, 256, 0, s>>>(g, kc, part);
+        else gemm_skinny_kernel<MT, false, EPI, false><<<grid, 256, 0, s>>>(g, kc, part);
         const int64_t total = (int64_t)g.M * g.N;
         splitk_reduce_kernel<EPI><<<(unsigned)std::min<int64_t>((total + 255) / 256, 1024), 256, 0, s>>>(g, ksplit, part);
     }
@@ -828,12 +871,18 @@ int launch_gemm_skinny_partial(const GemmArgs& g, float* part, hipStream_t s) {
     const int ks = skinny_ksplit(g.N, g.K);
     const dim3 grid((g.N + 63) / 64, ks, (g.M + 63) / 64);
     const int kc = g.K / ks;
-    switch ((g.M + 15) / 16) {
-        case 1: gemm_skinny_kernel<1, false, EPI_F32><<<grid, 256, 0, s>>>(g, kc, part); break;
-        case 2: gemm_skinny_kernel<2, false, EPI_F32><<<grid, 256, 0, s>>>(g, kc, part); break;
-        case 3: gemm_skinny_kernel<3, false, EPI_F32><<<grid, 256, 0, s>>>(g, kc, part); break;
-        default: gemm_skinny_kernel<4, false, EPI_F32><<<grid, 256, 0, s>>>(g, kc, part); break;
+#define OSW_SKINNY_PART(MT_)                                                                     \
+    do {                                                                                         \
+        if (g.A_lo) gemm_skinny_kernel<MT_, false, EPI_F32, true><<<grid, 256, 0, s>>>(g, kc, part);  \
+        else gemm_skinny_kernel<MT_, false, EPI_F32, false><<<grid, 256, 0, s>>>(g, kc, part);       \
+    } while (0)
+    switch (std::min(g.M, 64) <= 16 ? 1 : std::min(g.M, 64) <= 32 ? 2 : std::min(g.M, 64) <= 48 ? 3 : 4) {
+        case 1: OSW_SKINNY_PART(1); break;
+        case 2: OSW_SKINNY_PART(2); break;
+        case 3: OSW_SKINNY_PART(3); break;
+        default: OSW_SKINNY_PART(4); break;
     }
+#undef OSW_SKINNY_PART
     return ks;
 }
 
@@ -861,7 +910,8 @@ void launch_gemm_tiled_partial(const GemmArgs& g0, float* part, int ks, hipStrea
     g.bias = nullptr;
     g.epi = EPI_F32;
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, ks);
-    gemm_kernel<EPI_F32><<<grid, NTHR, 0, s>>>(g);
+    if (g.A_lo) gemm_kernel<EPI_F32, true><<<grid, NTHR, 0, s>>>(g);
+    else gemm_kernel<EPI_F32><<<grid, NTHR, 0, s>>>(g);
 }
 
 void launch_gemm_skinny(const GemmArgs& g, float* part, hipStream_t s) {
@@ -884,12 +934,19 @@ void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s) {
     static const bool no_wide = getenv("OSW_NO_WIDE") != nullptr;  // A/B switch
     const bool wide_ok = g.M <= WBM && g.epi == EPI_F32 && g.kc == 0 && g.c_grp_rows == g.M && g.K % BK == 0;
     if (wide_ok && (variant == 5 || (variant == 0 && g.N >= 16384 && !no_wide))) {
-        gemm_wide_kernel<<<(g.N + WBN - 1) / WBN, 256, 0, s>>>(g);
+        if (g.A_lo) gemm_wide_kernel<true><<<(g.N + WBN - 1) / WBN, 256, 0, s>>>(g);
+        else gemm_wide_kernel<false><<<(g.N + WBN - 1) / WBN, 256, 0, s>>>(g);
         return;
     }
     // big tile when it still yields >= 2 waves of workgroups over 256 CUs
     const int64_t big_tiles = (int64_t)((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
-    const bool big = variant == 2 || (variant == 0 && big_tiles >= 512 && g.N % 8 == 0 && !getenv("OSW_GEMM128"));
+    const bool big = !g.A_lo && (variant == 2 || (variant == 0 && big_tiles >= 512 && g.N % 8 == 0 &&
+                                                   !getenv("OSW_GEMM128")));
+    if (g.A_lo && g.epi == EPI_F32) {  // decoder (hi/lo activations): the 128-tile kernel, fp32 logits
+        dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
+        gemm_kernel<EPI_F32, true><<<grid, NTHR, 0, s>>>(g);
+        return;
+    }
     static const bool two_phase = getenv("OSW_GEMM_2PHASE") != nullptr;  // A/B switch for the 8-phase schedule
     if (variant == 4 || (variant == 0 && big && !two_phase)) {
         switch (g.epi) {

@@ -33,13 +33,17 @@ void launch_enc_attn(const h16*, h16*, int, int, int, hipStream_t);
 void launch_init_uniform(void*, bool, int64_t, uint64_t, float, float, int64_t, int64_t, hipStream_t);
 uint64_t hash_stream_key(uint64_t, int64_t);
 void launch_dec_embed(const h16*, const float*, const int*, const int*, int, int, int, float*, hipStream_t);
-void launch_dec_self_attn(const float*, int, const float*, h16*, h16*, const int*, int, int, int, h16*, const int*, int,
-                          hipStream_t);
-void launch_dec_cross_attn(const float*, int, const float*, const h16*, const h16*, int, int, int, int, h16*, float*,
-                           int*, hipStream_t);
-void launch_dec_resid_ln(const float*, int, int, int, const float*, float*, const float*, const float*, h16*,
+void launch_dec_self_attn(const float*, int, const float*, h16*, h16*, const int*, int, int, int, h16*, int64_t,
+                          const int*, int, hipStream_t);
+void launch_dec_cross_attn(const float*, int, const float*, const h16*, const h16*, int, int, int, int, h16*, int64_t,
+                           float*, int*, hipStream_t);
+void launch_dec_resid_ln(const float*, int, int, int, const float*, float*, const float*, const float*, h16*, int64_t,
                          const h16*, const float*, const int*, const int*, int, hipStream_t);
-void launch_dec_reduce_gelu(const float*, int, int, int, const float*, h16*, hipStream_t);
+void launch_dec_reduce_gelu(const float*, int, int, int, const float*, h16*, int64_t, hipStream_t);
+void launch_ingest_sumsq(const int16_t*, int, int, const int2*, int, float*, float*, hipStream_t);
+void launch_ingest_gain(const int16_t*, int64_t, int, int, float, int16_t*, hipStream_t);
+void launch_ingest_resample(const int16_t*, int64_t, const float*, int, int, int, int64_t, int64_t, int16_t*,
+                            hipStream_t);
 }  // namespace osw
 
 using namespace osw;
@@ -145,7 +149,8 @@ struct osw_ctx {
     float* X = nullptr;
     int n_encoded = 0;
 
-    // decoder workspace
+    // decoder workspace.  xdn / dattn / dh (the GEMM operands) are hi/lo fp16 pairs:
+    // the lo halves sit R rows after the hi halves (lo_off below)
     float* xd = nullptr;
     h16 *xdn = nullptr, *dqkv = nullptr, *dattn = nullptr, *dq = nullptr, *dh = nullptr, *kc = nullptr, *vc = nullptr;
     float* logits = nullptr;
@@ -405,11 +410,11 @@ void setup_workspace(osw_ctx* c) {
     c->XKV = dalloc<h16>((int64_t)d.n_text_layer * 2 * Me * Dd, o);
     const int64_t R = c->R;
     c->xd = dalloc<float>(R * Dd, o);
-    c->xdn = dalloc<h16>(R * Dd, o);
+    c->xdn = dalloc<h16>(2 * R * Dd, o);
     c->dqkv = dalloc<h16>(R * 3 * Dd, o);
-    c->dattn = dalloc<h16>(R * Dd, o);
+    c->dattn = dalloc<h16>(2 * R * Dd, o);
     c->dq = dalloc<h16>(R * Dd, o);
-    c->dh = dalloc<h16>(R * 4 * Dd, o);
+    c->dh = dalloc<h16>(2 * R * 4 * Dd, o);
     const int64_t kvn = (int64_t)d.n_text_layer * R * d.n_text_ctx * Dd;
     c->kc = dalloc<h16>(kvn, o);
     c->vc = dalloc<h16>(kvn, o);
@@ -466,6 +471,7 @@ bool skinny_ok(const GemmArgs& g) {
 
 void run_gemm(osw_ctx* c, const GemmArgs& g, int cls) {
     REQUIRE(g.K % 64 == 0, "GEMM K must be a multiple of 64");
+    REQUIRE(!g.A_lo || g.epi == EPI_F32, "hi/lo operands feed fp32 outputs only");
     Timed t(c, cls, 2.0 * g.M * g.N * g.K);
     if (skinny_ok(g)) {
         REQUIRE((int64_t)skinny_ksplit(g.N, g.K) * g.M * g.N <= c->part_floats, "split-K workspace too small");
@@ -562,53 +568,61 @@ void decoder_step(osw_ctx* c, int nb, int group, bool gather) {
     const int64_t kv_layer = (int64_t)nb * H * ctx * 64;
     REQUIRE(nb <= c->R && D <= 1280, "decoder step: rows <= capacity and D <= 1280");
     REQUIRE(ctx <= 448, "decoder self-attention holds at most 448 positions");
+    // the decoder's GEMM operands are hi/lo fp16 pairs (fp32-accurate activations: the
+    // logits stay within 1e-3 of an fp32 decoder); lo = hi + R rows
+    const int64_t lo_d = (int64_t)c->R * D, lo_4d = (int64_t)c->R * 4 * D;
     // <= 64 rows: split-K skinny GEMM; more (beam search): see below
     auto partial = [&](const h16* A, int lda, const h16* Wt, int N, int K) {
+        const int64_t lo = lda == 4 * D ? lo_4d : lo_d;
         // > 64 rows, N > 1536: 128x128 split-K tiles; N <= 1536: skinny row groups (measured
         // at 320 rows: N = 1280 11.4 vs 12.8 us, N = 3840 17.9 vs 12.8, N = 5120 21.7 vs 20.4)
         static const int force = getenv("OSW_BEAM_GEMM") ? atoi(getenv("OSW_BEAM_GEMM")) : 0;  // 1 tiled, 2 skinny
         if (nb > 64 && (force == 1 || (force == 0 && N > 1536))) {
             const int ks = tiled_ksplit(nb, N, K);
             REQUIRE((int64_t)ks * nb * N <= c->part_floats, "decoder workspace too small");
-            launch_gemm_tiled_partial(gemm_plain(A, lda, Wt, nullptr, nb, N, K, nullptr, 0, EPI_F32), c->part, ks,
-                                      c->stream);
+            GemmArgs g = gemm_plain(A, lda, Wt, nullptr, nb, N, K, nullptr, 0, EPI_F32);
+            g.A_lo = A + lo;
+            launch_gemm_tiled_partial(g, c->part, ks, c->stream);
             return ks;
         }
         GemmArgs g = gemm_plain(A, lda, Wt, nullptr, nb, N, K, nullptr, 0, EPI_F32);
+        g.A_lo = A + lo;
         REQUIRE((int64_t)skinny_ksplit(N, K) * nb * N <= c->part_floats, "split-K workspace too small");
         return launch_gemm_skinny_partial(g, c->part, c->stream);
     };
     // x = tok_emb[tok] + pos_emb[pos]; xdn = LN1_0(x)
-    launch_dec_resid_ln(nullptr, 0, nb, D, nullptr, c->xd, WF(c, "dec.l0.ln1.g"), WF(c, "dec.l0.ln1.b"), c->xdn,
+    launch_dec_resid_ln(nullptr, 0, nb, D, nullptr, c->xd, WF(c, "dec.l0.ln1.g"), WF(c, "dec.l0.ln1.b"), c->xdn, lo_d,
                         WH(c, "dec.tok"), WF(c, "dec.pos"), c->cur_tok, c->pos, ctx, c->stream);
     for (int l = 0; l < L; ++l) {
         const std::string p = "dec.l" + std::to_string(l);
         int ks = partial(c->xdn, D, WH(c, p + ".qkv.w"), 3 * D, D);
         launch_dec_self_attn(c->part, ks, WF(c, p + ".qkv.b"), c->kc + l * kv_layer, c->vc + l * kv_layer, c->pos, nb,
-                             H, ctx, c->dattn, gather ? c->anc : nullptr, group, c->stream);
+                             H, ctx, c->dattn, lo_d, gather ? c->anc : nullptr, group, c->stream);
         ks = partial(c->dattn, D, WH(c, p + ".o.w"), D, D);
         launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".o.b"), c->xd, WF(c, p + ".ln2.g"), WF(c, p + ".ln2.b"),
-                            c->xdn, nullptr, nullptr, nullptr, nullptr, ctx, c->stream);
+                            c->xdn, lo_d, nullptr, nullptr, nullptr, nullptr, ctx, c->stream);
         ks = partial(c->xdn, D, WH(c, p + ".xq.w"), D, D);
         {
             Timed t(c, CL_XATTN, 2.0 * nb * H * (double)T_ENC * 64 * 2);
             launch_dec_cross_attn(c->part, ks, WF(c, p + ".xq.b"), c->XKV + (2 * l) * xkv_which,
-                                  c->XKV + (2 * l + 1) * xkv_which, nb, H, T_ENC, group, c->dattn, c->xws,
+                                  c->XKV + (2 * l + 1) * xkv_which, nb, H, T_ENC, group, c->dattn, lo_d, c->xws,
                                   c->xticket, c->stream);
         }
         ks = partial(c->dattn, D, WH(c, p + ".xo.w"), D, D);
         launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".xo.b"), c->xd, WF(c, p + ".ln3.g"), WF(c, p + ".ln3.b"),
-                            c->xdn, nullptr, nullptr, nullptr, nullptr, ctx, c->stream);
+                            c->xdn, lo_d, nullptr, nullptr, nullptr, nullptr, ctx, c->stream);
         // (a whole-K fc1 with the GELU epilogue fused has only N/64 = 80 workgroups at
         // turbo: 22.7 us vs 9.6 + 4.7 us for split-K + reduce, measured)
         ks = partial(c->xdn, D, WH(c, p + ".fc1.w"), 4 * D, D);
-        launch_dec_reduce_gelu(c->part, ks, nb, 4 * D, WF(c, p + ".fc1.b"), c->dh, c->stream);
+        launch_dec_reduce_gelu(c->part, ks, nb, 4 * D, WF(c, p + ".fc1.b"), c->dh, lo_4d, c->stream);
         ks = partial(c->dh, 4 * D, WH(c, p + ".fc2.w"), D, 4 * D);
         const std::string nx = l + 1 < L ? "dec.l" + std::to_string(l + 1) + ".ln1" : std::string("dec.lnpost");
         launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".fc2.b"), c->xd, WF(c, nx + ".g"), WF(c, nx + ".b"), c->xdn,
-                            nullptr, nullptr, nullptr, nullptr, ctx, c->stream);
+                            lo_d, nullptr, nullptr, nullptr, nullptr, ctx, c->stream);
     }
-    run_gemm(c, gemm_plain(c->xdn, D, WH(c, "dec.tok"), nullptr, nb, d.n_vocab, D, c->logits, d.n_vocab, EPI_F32), 0);
+    GemmArgs gl = gemm_plain(c->xdn, D, WH(c, "dec.tok"), nullptr, nb, d.n_vocab, D, c->logits, d.n_vocab, EPI_F32);
+    gl.A_lo = c->xdn + lo_d;
+    run_gemm(c, gl, 0);
 }
 
 void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) {
@@ -849,6 +863,101 @@ void log_mel(osw_ctx* c, const int16_t* pcm, const int64_t* offsets, int n, int 
     c->n_clips = n;
     if (nf_out)
         for (int i = 0; i < n; ++i) nf_out[i] = c->nframes[i];
+}
+
+// ------------------------------ ingest --------------------------------------
+// Per-device state of the context-free ingest entry points (osw_ingest_*): a stream
+// and scratch buffers grown on demand, one mutex per device.
+struct IngestDev {
+    std::mutex mu;
+    hipStream_t s = nullptr;
+    std::vector<void*> owned;
+    int16_t* in = nullptr;
+    size_t in_cap = 0;
+    int16_t* out = nullptr;
+    size_t out_cap = 0;
+    float* sums = nullptr;   // [full blocks | tail leaves]
+    size_t sums_cap = 0;
+    int2* leaves = nullptr;  // tail leaves (<= 128)
+    float* taps = nullptr;
+    size_t taps_cap = 0;
+};
+std::mutex g_ingest_mu;
+std::map<int, std::unique_ptr<IngestDev>> g_ingest;
+
+IngestDev& ingest_dev(int device) {
+    std::lock_guard<std::mutex> lk(g_ingest_mu);
+    auto& p = g_ingest[device];
+    if (!p) {
+        int ndev = 0;
+        HIPCHK(hipGetDeviceCount(&ndev));
+        REQUIRE(device >= 0 && device < ndev, "device ordinal out of range");
+        p.reset(new IngestDev());
+        HIPCHK(hipSetDevice(device));
+        HIPCHK(hipStreamCreateWithFlags(&p->s, hipStreamNonBlocking));
+        p->leaves = dalloc<int2>(128, p->owned);
+    }
+    return *p;
+}
+
+template <typename T>
+T* grow(T*& ptr, size_t& cap, size_t n, std::vector<void*>& owned) {
+    if (n > cap) {
+        cap = n + n / 2 + 1024;
+        ptr = dalloc<T>(cap, owned);   // old buffer stays owned until the process exits (rare growth)
+    }
+    return ptr;
+}
+
+// numpy FLOAT_pairwise_sum tree of one block of n elements: leaves in order
+void pw_leaves(int64_t off, int64_t n, std::vector<int2>& out) {
+    if (n <= 128) {
+        out.push_back(make_int2((int)off, (int)n));
+        return;
+    }
+    int64_t n2 = n / 2;
+    n2 -= n2 % 8;
+    pw_leaves(off, n2, out);
+    pw_leaves(off + n2, n - n2, out);
+}
+// the same tree combining the leaf sums (float32 adds, left + right)
+float pw_combine(int64_t n, const float*& leaf) {
+    if (n <= 128) return *leaf++;
+    int64_t n2 = n / 2;
+    n2 -= n2 % 8;
+    const float a = pw_combine(n2, leaf);
+    const float b = pw_combine(n - n2, leaf);
+    return a + b;
+}
+
+// numpy: np.mean(np.square(mono(pcm) / 32768)) as float32, bit for bit
+float ingest_mean_square(IngestDev& g, const int16_t* pcm, int64_t n, int ch) {
+    const int64_t full = n / 8192, tail = n % 8192;
+    std::vector<int2> lv;
+    if (tail) pw_leaves(0, tail, lv);
+    REQUIRE(lv.size() <= 128, "tail leaves");
+    const size_t ns = (size_t)full + lv.size();
+    grow(g.sums, g.sums_cap, ns + 1, g.owned);
+    if (!lv.empty()) HIPCHK(hipMemcpyAsync(g.leaves, lv.data(), lv.size() * sizeof(int2), hipMemcpyHostToDevice, g.s));
+    launch_ingest_sumsq(pcm, ch, (int)full, g.leaves, (int)lv.size(), g.sums, g.sums + full, g.s);
+    HIPCHK(hipGetLastError());
+    std::vector<float> h(ns);
+    if (ns) HIPCHK(hipMemcpyAsync(h.data(), g.sums, ns * 4, hipMemcpyDeviceToHost, g.s));
+    HIPCHK(hipStreamSynchronize(g.s));
+    // np.add.reduce: the 8192-element blocks' pairwise sums added in order
+    float acc = 0.f;
+    for (int64_t b = 0; b < full; ++b) acc = b == 0 ? h[0] : acc + h[b];
+    if (tail) {
+        const float* p = h.data() + full;
+        const float t = pw_combine(tail, p);
+        acc = full ? acc + t : t;
+    }
+    return acc / (float)n;
+}
+
+int64_t upfirdn_output_len(int64_t len_h, int64_t n_in, int64_t up, int64_t down) {
+    const int64_t nt = (n_in + (len_h + ((up - len_h % up) % up)) / up - 1) * up;
+    return nt / down + (nt % down ? 1 : 0);
 }
 
 }  // namespace
@@ -1192,5 +1301,74 @@ int osw_get_profile(osw_ctx* c, osw_profile* out) {
 }
 
 void* osw_stream(osw_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int osw_ingest_mean_square(int32_t device, const int16_t* pcm, int64_t n_frames, int32_t channels, float* out_mean) {
+    return guard([&] {
+        REQUIRE(pcm && out_mean, "null argument");
+        REQUIRE(n_frames >= 1 && channels >= 1 && channels <= 64, "bad PCM shape");
+        IngestDev& g = ingest_dev(device);
+        std::lock_guard<std::mutex> lk(g.mu);
+        HIPCHK(hipSetDevice(device));
+        const size_t n = (size_t)n_frames * channels;
+        grow(g.in, g.in_cap, n, g.owned);
+        HIPCHK(hipMemcpyAsync(g.in, pcm, n * 2, hipMemcpyHostToDevice, g.s));
+        *out_mean = ingest_mean_square(g, g.in, n_frames, channels);
+    });
+}
+
+int osw_ingest_apply_gain(int32_t device, const int16_t* pcm, int64_t n_frames, int32_t channels, int32_t apply_gain,
+                          float gain, int16_t* out) {
+    return guard([&] {
+        REQUIRE(pcm && out, "null argument");
+        REQUIRE(n_frames >= 1 && channels >= 1 && channels <= 64, "bad PCM shape");
+        IngestDev& g = ingest_dev(device);
+        std::lock_guard<std::mutex> lk(g.mu);
+        HIPCHK(hipSetDevice(device));
+        const size_t n = (size_t)n_frames * channels;
+        grow(g.in, g.in_cap, n, g.owned);
+        grow(g.out, g.out_cap, (size_t)n_frames, g.owned);
+        HIPCHK(hipMemcpyAsync(g.in, pcm, n * 2, hipMemcpyHostToDevice, g.s));
+        launch_ingest_gain(g.in, n_frames, channels, apply_gain, gain, g.out, g.s);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(out, g.out, (size_t)n_frames * 2, hipMemcpyDeviceToHost, g.s));
+        HIPCHK(hipStreamSynchronize(g.s));
+    });
+}
+
+int osw_ingest_resample(int32_t device, const int16_t* pcm, int64_t n_in, int32_t up, int32_t down, const float* h,
+                        int32_t n_h, int16_t* out, int64_t n_out) {
+    return guard([&] {
+        REQUIRE(pcm && h && out, "null argument");
+        REQUIRE(n_in >= 2 && up >= 1 && down >= 1 && n_h >= 1 && (n_h & 1), "bad resample arguments");
+        const int64_t want = (n_in * up) / down + ((n_in * up) % down ? 1 : 0);
+        REQUIRE(n_out == want, "n_out must be ceil(n_in * up / down)");
+        // resample_poly's zero padding of the filter (scipy/signal/_signaltools.py)
+        const int64_t half_len = (n_h - 1) / 2;
+        const int64_t pre = down - half_len % down;
+        const int64_t pre_remove = (half_len + pre) / down;
+        int64_t post = 0;
+        while (upfirdn_output_len(n_h + pre + post, n_in, up, down) < n_out + pre_remove) ++post;
+        const int64_t len_h = n_h + pre + post;
+        const int64_t padlen = len_h + (up - len_h % up) % up;
+        const int64_t hpp = padlen / up;
+        // _pad_h: htf[p * hpp + j] = h_full[(hpp - 1 - j) * up + p]
+        std::vector<float> full((size_t)padlen, 0.f), htf((size_t)padlen);
+        for (int64_t i = 0; i < n_h; ++i) full[(size_t)(pre + i)] = h[i];
+        for (int64_t p = 0; p < up; ++p)
+            for (int64_t j = 0; j < hpp; ++j) htf[(size_t)(p * hpp + j)] = full[(size_t)((hpp - 1 - j) * up + p)];
+        IngestDev& g = ingest_dev(device);
+        std::lock_guard<std::mutex> lk(g.mu);
+        HIPCHK(hipSetDevice(device));
+        grow(g.in, g.in_cap, (size_t)n_in, g.owned);
+        grow(g.out, g.out_cap, (size_t)n_out, g.owned);
+        grow(g.taps, g.taps_cap, (size_t)padlen, g.owned);
+        HIPCHK(hipMemcpyAsync(g.in, pcm, (size_t)n_in * 2, hipMemcpyHostToDevice, g.s));
+        HIPCHK(hipMemcpyAsync(g.taps, htf.data(), htf.size() * 4, hipMemcpyHostToDevice, g.s));
+        launch_ingest_resample(g.in, n_in, g.taps, (int)hpp, up, down, pre_remove, n_out, g.out, g.s);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(out, g.out, (size_t)n_out * 2, hipMemcpyDeviceToHost, g.s));
+        HIPCHK(hipStreamSynchronize(g.s));
+    });
+}
 
 }  // extern "C"

@@ -115,6 +115,9 @@ def write_model_bin(path: str, variables: dict, aliases: dict | None = None, spe
 
 def _get(v: dict, aliases: dict, name: str) -> np.ndarray:
     name = aliases.get(name, name)
+    if name not in v:
+        raise ValueError(f"CTranslate2 model.bin has no variable {name!r}, which the Whisper spec requires "
+                         f"(found {len(v)} variables, e.g. {sorted(v)[:3]})")
     x = v[name]
     sc = v.get(name + "_scale")
     if x.dtype == np.int8 and sc is not None:  # per-row int8 quantisation
@@ -123,6 +126,10 @@ def _get(v: dict, aliases: dict, name: str) -> np.ndarray:
 
 
 def dims_from_ct2(v: dict) -> WhisperDims:
+    for k in ("encoder/conv1/weight", "decoder/embeddings/weight", "decoder/position_encodings/encodings",
+              "encoder/position_encodings/encodings"):
+        if k not in v:
+            raise ValueError(f"not a CTranslate2 Whisper model.bin: no {k!r}")
     D, n_mels, _ = v["encoder/conv1/weight"].shape
     import re
 

@@ -8,7 +8,8 @@ here becomes a request on a queue; one worker thread per GPU drains up to
 arrives), runs them as one batched seek loop on its engine, and completes each
 caller's future.  Requests are routed to the worker with the shortest queue
 (multi-GPU serving: independent clips, no collective).  A worker whose GPU fails
-marks itself dead and re-queues what it held on the survivors.
+marks every worker of that GPU (its sibling lanes) dead and re-queues the requests
+it held that are still unanswered on the workers of the other GPUs.
 """
 from __future__ import annotations
 
@@ -63,11 +64,11 @@ class _Worker(threading.Thread):
             try:
                 self._run_batch(batch)
             except Exception as e:  # noqa: BLE001 - forwarded to callers
-                if self.pool.is_device_error(e) and len(self.pool.workers) > 1:
-                    self.alive = False
+                if self.pool.is_device_error(e) and self.pool.fail_device(self):
+                    # requests of earlier opts-groups of this batch are already answered
                     for r in batch:
-                        self.pool.submit_req(r, exclude=self)
-                    self.pool.drain_dead(self)
+                        if not r.fut.done():
+                            self.pool.submit_req(r)
                     return
                 for r in batch:
                     if not r.fut.done():
@@ -83,7 +84,8 @@ class _Worker(threading.Thread):
             res = transcribe_clips(self.engine, [r.pcm for r in reqs], reqs[0].opts, self.pool.tokenizer,
                                    self.pool.suppress_for(reqs[0].opts))
             for r, out in zip(reqs, res):
-                r.fut.set_result(out)
+                if not r.fut.done():
+                    r.fut.set_result(out)
 
 
 class BatchRunner:
@@ -104,14 +106,39 @@ class BatchRunner:
 
     @staticmethod
     def is_device_error(e: Exception) -> bool:
+        from ._lib import OswDeviceError
+        if isinstance(e, OswDeviceError):
+            return True
         s = str(e)
         return "hipError" in s or "(-100)" in s
+
+    @staticmethod
+    def _device_of(w: _Worker):
+        return getattr(w.engine, "device", None)
+
+    def fail_device(self, failed: _Worker) -> bool:
+        """Mark every worker on `failed`'s GPU dead (lanes share the device) and move their
+        queued requests to the survivors.  False when no other GPU's worker is alive
+        (the error then goes to the callers)."""
+        dev = self._device_of(failed)
+        same = [w for w in self.workers if w is failed or (dev is not None and self._device_of(w) == dev)]
+        with self._lock:
+            if not any(w.alive and w not in same for w in self.workers):
+                return False
+            for w in same:
+                w.alive = False
+        for w in same:
+            self.drain_dead(w)
+            if w is not failed:
+                w.q.put(None)   # its thread exits after the batch it may be running
+        return True
 
     def submit_req(self, r: _Req, exclude=None) -> None:
         with self._lock:
             live = [w for w in self.workers if w.alive and w is not exclude]
             if not live:
-                r.fut.set_exception(RuntimeError("no live GPU worker"))
+                if not r.fut.done():
+                    r.fut.set_exception(RuntimeError("no live GPU worker"))
                 return
             w = min(live, key=lambda x: x.load())
             w.q.put(r)
@@ -122,7 +149,7 @@ class BatchRunner:
                 r = dead.q.get_nowait()
             except queue.Empty:
                 return
-            if r is not None:
+            if r is not None and not r.fut.done():
                 self.submit_req(r, exclude=dead)
 
     def submit(self, pcm: np.ndarray, opts: TranscribeOptions) -> Future:
@@ -135,7 +162,8 @@ class BatchRunner:
 
     def close(self) -> None:
         for w in self.workers:
-            w.q.put(None)
+            if w.is_alive():
+                w.q.put(None)
         for w in self.workers:
             w.join(timeout=30)
         for w in self.workers:

@@ -7,7 +7,8 @@ k_proj without bias), ``:566-642`` (encoder), ``:649-790`` (decoder), ``:965-970
 ``open-speech_amd/weights.py``.
 
 ``fp16=True`` rounds activations to fp16 at exactly the points where the HIP path
-stores fp16 (GEMM inputs, attention probabilities fed to the MFMA, K/V caches), with
+stores fp16 (``GPU_POINTS``: encoder GEMM inputs, attention probabilities fed to the
+MFMA, K/V caches, decoder q), with
 fp32 accumulation everywhere and an fp32 residual stream, so the comparison with
 the GPU isolates accumulation-order effects.  ``fp16=False`` is plain fp32/fp64 math
 and is what transformers' fp32 model computes.  ``fp16`` may also be a collection of
@@ -24,12 +25,17 @@ def _h(x, on=True):
     return x.astype(np.float16).astype(np.float32) if on else x.astype(np.float32)
 
 
-# every place the HIP path stores an activation in fp16
+# every place an fp16 Whisper pipeline may store an activation in fp16
 ROUND_POINTS = frozenset({
     "mel", "conv1", "enc_ln", "enc_qkv", "enc_p", "enc_attn", "enc_fc1", "enc_out",  # encoder
     "xkv",                                                                           # cross K/V
     "dec_ln", "dec_qkv", "dec_attn", "dec_q", "dec_fc1", "dec_final_ln",             # decoder
 })
+# the points where the HIP path DOES round: the decoder's GEMM operands
+# (LayerNorm outputs, attention outputs, GELU outputs) are hi/lo fp16 pairs, i.e. fp32-
+# accurate, because rounding them cost 1.5e-3 of log-softmax at turbo dims
+# (tools/precision_study.py); q, the self-K/V cache and the cross-K/V stay fp16.
+GPU_POINTS = ROUND_POINTS - {"dec_ln", "dec_attn", "dec_fc1", "dec_final_ln"}
 
 
 def layer_norm(x, g, b, eps=1e-5):
@@ -65,7 +71,7 @@ class WhisperOracle:
     def __init__(self, dims, weights: dict, fp16=True):
         self.d = dims
         if fp16 is True or fp16 is False:
-            self.points = ROUND_POINTS if fp16 else frozenset()
+            self.points = GPU_POINTS if fp16 else frozenset()
         else:
             self.points = frozenset(fp16)
             assert self.points <= ROUND_POINTS, self.points - ROUND_POINTS

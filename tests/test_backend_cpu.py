@@ -302,3 +302,68 @@ def test_wav_stereo_and_resample():
 def test_non_wav_rejected_or_converted():
     with pytest.raises(ValueError):
         decode_audio_bytes(b"RIFF" + b"\x00" * 100)   # the reference tests' fake upload
+
+
+# --------------------------------------------------------------------------- failover
+def test_device_error_fails_over_to_other_gpu():
+    """A HIP error in the second opts-group of a batch: the first group's answers stand,
+    only the unanswered requests move, and they skip the failed GPU's sibling lane
+    (runner.py re-queued answered requests onto a lane of the same GPU)."""
+    from open_speech_amd._lib import OswDeviceError
+    from open_speech_amd.runner import BatchRunner
+    from open_speech_amd.segments import TranscribeOptions
+    from open_speech_amd.tokenizer import WhisperTokenizer
+
+    class Eng(FakeEngine):
+        def __init__(self, device, tag, fail_on_call=None):
+            super().__init__(D.MICRO_TEST, device, 8,
+                             lambda w, i, p, l: WindowOutput([TB, 1000 + tag, TB + 50], -1.0, 0.01, ST.first_lang))
+            self.device, self.tag, self.fail_on_call, self.n_decode = device, tag, fail_on_call, 0
+
+        def decode(self, n, cfg, prefix=None, dump_steps=0, languages=None):
+            self.n_decode += 1
+            if self.n_decode == self.fail_on_call:
+                raise OswDeviceError("osw_decode_windows failed (-100): hipErrorLaunchFailure", -100)
+            return super().decode(n, cfg, prefix, dump_steps, languages)
+
+    a, a2, b = Eng(0, 1, fail_on_call=2), Eng(0, 2), Eng(1, 3)
+    runner = BatchRunner([a, a2, b], WhisperTokenizer(51866), max_wait_ms=300)
+    try:
+        from concurrent.futures import Future
+        from open_speech_amd.runner import _Req
+        reqs = []
+        for i in range(4):
+            opts = TranscribeOptions(beam_size=1, language="en" if i < 2 else "de")
+            reqs.append(_Req(synth.chirp_clip(i, 4.0), opts, Future()))
+        for r in reqs:
+            runner.workers[0].q.put(r)
+        res = [r.fut.result(timeout=30) for r in reqs]
+        assert [sg.tokens for sg in res[0].segments] == [[TB, 1001, TB + 50]]   # group 1 answered by GPU 0
+        assert all(sg.tokens == [TB, 1003, TB + 50] for r in res[2:] for sg in r.segments)  # moved to GPU 1
+        assert not runner.workers[0].alive and not runner.workers[1].alive and runner.workers[2].alive
+        assert a2.n_decode == 0
+        # new work avoids the failed GPU
+        assert [sg.tokens for sg in runner.transcribe(synth.chirp_clip(9, 3.0), TranscribeOptions(beam_size=1,
+                language="en")).segments] == [[TB, 1003, TB + 50]]
+    finally:
+        runner.close()
+
+
+def test_cache_listing_with_stt_model_dir(tmp_path, monkeypatch):
+    """STT_MODEL_DIR holds HF-style and plainly named model dirs (reference
+    src/backends/faster_whisper.py:122-195): both are listed, found and deletable."""
+    (tmp_path / "models--Systran--faster-whisper-base" / "snapshots" / "x").mkdir(parents=True)
+    (tmp_path / "models--Systran--faster-whisper-base" / "snapshots" / "x" / "model.bin").write_bytes(b"\0" * 2048)
+    (tmp_path / "my-turbo").mkdir()
+    (tmp_path / "my-turbo" / "model.bin").write_bytes(b"\0" * 4096)
+    (tmp_path / ".hidden").mkdir()
+    monkeypatch.setenv("STT_MODEL_DIR", str(tmp_path))
+    b = make_backend()
+    ids = {m["model"] for m in b.list_cached_models()}
+    assert ids == {"Systran/faster-whisper-base", "my-turbo"}
+    assert b.is_model_cached("Systran/faster-whisper-base") and b.is_model_cached("org/my-turbo")
+    assert b.delete_cached_model("my-turbo") and not (tmp_path / "my-turbo").exists()
+    monkeypatch.delenv("STT_MODEL_DIR")
+    monkeypatch.setenv("HF_HUB_CACHE", str(tmp_path))
+    b2 = make_backend()
+    assert {m["model"] for m in b2.list_cached_models()} == {"Systran/faster-whisper-base"}

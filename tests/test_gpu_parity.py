@@ -282,6 +282,35 @@ def test_sibling_shares_weights(tiny_engine):
         sib.close()
 
 
+def test_sibling_beam_concurrent_is_deterministic(tiny_engine):
+    """Beam-5 (the reference default, 5 decoder rows per window: the NB = 5 cross-attention
+    with v_dot2 scores and the LDS P·V reduction) on two lanes at once: parent and sibling
+    give bit-identical tokens and sum_logprob to a lone run."""
+    import threading
+    d, eng, w = tiny_engine
+    sib = eng.sibling(max_batch=2)
+    try:
+        sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+        cfg = DecodeConfig(suppress_tokens=sup, max_length=64, beam_size=5)
+        clips = [synth.chirp_clip(33, 30.0), synth.chirp_clip(34, 17.0)]
+        ref = eng.transcribe_batch(clips, cfg)
+        got = {}
+
+        def run(name, e):
+            got[name] = [e.transcribe_batch(clips, cfg) for _ in range(3)]
+
+        th = [threading.Thread(target=run, args=(n, e)) for n, e in (("a", eng), ("b", sib))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        for outs in got["a"] + got["b"]:
+            for x, y in zip(outs, ref):
+                assert x.tokens == y.tokens and x.sum_logprob == y.sum_logprob
+    finally:
+        sib.close()
+
+
 def test_sampling_draws_match_oracle(tiny_engine):
     """temperature > 0: every pick is argmax(x / T + Gumbel(seed, row, step, token)) over
     the rule-masked logits.  Replayed by the oracle on the GPU's own logits: ids exact;

@@ -188,6 +188,94 @@ def gen_turbo_layer(out):
     return {"w_seed": TURBO_LAYER_SEED, "x_seed": 4242}
 
 
+TURBO_SEED = 0          # the bench's init_random(seed=0) weights
+TURBO_CLIP = 0          # synth.chirp_clip(0, 30 s)
+TURBO_FULL_STEPS = 4    # full-vocabulary fp32 logits stored for the first steps
+TURBO_SUBSET = 256      # per step: logits of the top-32 tokens and of a fixed token sample
+
+
+def gen_turbo(out):
+    """whisper-large-v3-turbo end to end in fp32 (transformers): the encoder output
+    (selected rows + every row norm), the <|startoftranscript|> logits, and greedy
+    decoding to <|endoftext|> or 448 positions with the openai / faster-whisper
+    logits rules — ids, the chosen tokens' log-probs, top-5 per step, and per step
+    the log-sum-exp plus the logits of the top-32 and of a fixed token sample (so a
+    log-softmax check covers every step without storing 51866 floats per step)."""
+    d = D.LARGE_V3_TURBO
+    st = D.SpecialTokens.for_vocab(d.n_vocab)
+    w = weights.random_weights(d, seed=TURBO_SEED)
+    model = build_model(d, w)
+    del w
+    pcm = synth.chirp_clip(TURBO_CLIP, 30.0)
+    mel = fe_mel(pcm, d.n_mels)[:, :3000]
+    with torch.no_grad():
+        enc = model.model.encoder(input_features=torch.from_numpy(mel)[None]).last_hidden_state
+    tok = WhisperTokenizer(d.n_vocab)
+    suppress = get_suppressed_tokens(tok, [-1])
+    gc = GenerationConfig(no_timestamps_token_id=st.no_timestamps, eos_token_id=st.eot,
+                          max_initial_timestamp_index=50)
+
+    def step(ids, past):
+        with torch.no_grad():
+            o = model(encoder_outputs=(enc,), decoder_input_ids=torch.tensor([ids]), past_key_values=past,
+                      use_cache=True)
+        return o.logits[0, -1].double(), o.past_key_values
+
+    lg, past = step([st.sot], None)
+    sot_logits = lg.float().numpy().copy()
+    lang = st.first_lang + int(np.argmax(sot_logits[st.first_lang:st.first_lang + st.n_langs]))
+    nsp = float(torch.softmax(lg, -1)[st.no_speech])
+    prompt = [st.sot, lang, st.transcribe]
+    lg, past = step([lang], past)
+    lg, past = step([st.transcribe], past)
+    begin = len(prompt)
+    procs = [SuppressTokensAtBeginLogitsProcessor([st.blank, st.eot], begin),
+             SuppressTokensLogitsProcessor(list(suppress)),
+             WhisperTimeStampLogitsProcessor(gc, begin)]
+    sample = np.sort(np.random.default_rng(2024).choice(d.n_vocab, TURBO_SUBSET, replace=False)).astype(np.int32)
+    seq = list(prompt)
+    ids, lps, top5i, top5v, full, lse, sub_i, sub_v, margins = [], [], [], [], [], [], [], [], []
+    sum_lp = 0.0
+    while True:
+        raw = lg.float().numpy()
+        if len(full) < TURBO_FULL_STEPS:
+            full.append(raw.copy())
+        lse.append(float(torch.logsumexp(lg, -1)))
+        t32 = np.argsort(-raw, kind="stable")[:32].astype(np.int32)
+        sub_i.append(np.concatenate([t32, sample]))
+        sub_v.append(raw[sub_i[-1]])
+        x = lg[None].clone().float()
+        for p in procs:
+            x = p(torch.tensor([seq]), x)
+        lsm = torch.log_softmax(x.double(), -1)[0]
+        top2 = torch.topk(x[0], 2).values
+        margins.append(float(top2[0] - top2[1]))
+        nxt = int(torch.argmax(x[0]))
+        v, i = torch.topk(lg.float(), 5)
+        top5i.append(i.numpy())
+        top5v.append(v.numpy())
+        sum_lp += float(lsm[nxt])
+        lps.append(float(lsm[nxt]))
+        if nxt == st.eot:
+            break
+        ids.append(nxt)
+        seq.append(nxt)
+        if len(seq) >= d.n_text_ctx:
+            break
+        lg, past = step([nxt], past)
+    e = enc[0].numpy()
+    rows = np.r_[0:8, 700:708, 1492:1500]
+    np.savez_compressed(os.path.join(out, "turbo_model.npz"), enc_rows=rows, enc=e[rows].astype(np.float32),
+                        enc_rownorm=np.linalg.norm(e.astype(np.float64), axis=1), sot_logits=sot_logits,
+                        full_logits=np.stack(full), lse=np.array(lse), sub_ids=np.stack(sub_i), sub_vals=np.stack(sub_v),
+                        ids=np.array(ids, np.int32), logprobs=np.array(lps), top5_ids=np.stack(top5i).astype(np.int32),
+                        top5_vals=np.stack(top5v), margins=np.array(margins), language=np.int32(lang),
+                        no_speech_prob=np.float64(nsp), sum_logprob=np.float64(sum_lp))
+    print("turbo: lang", lang, "n_ids", len(ids), "first", ids[:12], "min margin", min(margins))
+    return {"seed": TURBO_SEED, "clip": TURBO_CLIP, "language": lang, "n_ids": len(ids),
+            "min_top2_margin": min(margins)}
+
+
 def gen_logits_rules(out):
     """Crafted token histories through transformers' Whisper processors."""
     st = D.SpecialTokens.for_vocab(51866)
@@ -235,15 +323,25 @@ def gen_logits_rules(out):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "tests", "golden"))
+    ap.add_argument("--only", default=None, help="comma list of: mel,rules,tiny,turbo_layer,turbo")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     torch.manual_seed(0)
-    meta = {"generator": "tools/make_golden.py", "transformers": __import__("transformers").__version__,
-            "torch": torch.__version__}
-    meta["mel"] = gen_mel(a.out)
-    meta["logits_rules"] = gen_logits_rules(a.out)
-    meta["tiny"] = gen_tiny(a.out)
-    meta["turbo_layer"] = gen_turbo_layer(a.out)
+    mp = os.path.join(a.out, "meta.json")
+    meta = json.load(open(mp)) if os.path.exists(mp) else {}
+    meta.update({"generator": "tools/make_golden.py", "transformers": __import__("transformers").__version__,
+                 "torch": torch.__version__})
+    only = set(a.only.split(",")) if a.only else {"mel", "rules", "tiny", "turbo_layer", "turbo"}
+    if "mel" in only:
+        meta["mel"] = gen_mel(a.out)
+    if "rules" in only:
+        meta["logits_rules"] = gen_logits_rules(a.out)
+    if "tiny" in only:
+        meta["tiny"] = gen_tiny(a.out)
+    if "turbo_layer" in only:
+        meta["turbo_layer"] = gen_turbo_layer(a.out)
+    if "turbo" in only:
+        meta["turbo"] = gen_turbo(a.out)
     with open(os.path.join(a.out, "meta.json"), "w") as fh:
         json.dump(meta, fh, indent=1)
 

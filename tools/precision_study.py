@@ -106,7 +106,8 @@ def main():
             report(nm, WhisperOracle(d, w, fp16=pts), enc=enc32)
         return
     encs = {}
-    encs["all"] = report("all points (GPU today)", WhisperOracle(d, w, fp16=True))
+    encs["all"] = report("all points (round-1 GPU)", WhisperOracle(d, w, fp16=ROUND_POINTS))
+    report("GPU points (hi/lo decoder)", WhisperOracle(d, w, fp16=True))
     report("encoder points only", WhisperOracle(d, w, fp16=ENC_POINTS))
     report("decoder points only", WhisperOracle(d, w, fp16=DEC_POINTS), enc=enc32)
     for p in ENC_POINTS:

@@ -48,12 +48,19 @@ def parse():
                          "(measured, 12 steps x 2 runs: 2 lanes 4023, 3 lanes 4234, 4 lanes 4057 audio-s/s)")
     ap.add_argument("--model", default="large-v3-turbo", choices=sorted(D.PRESETS))
     ap.add_argument("--max-length", type=int, default=448)
-    ap.add_argument("--latency-repeats", type=int, default=5)
+    ap.add_argument("--latency-repeats", type=int, default=50,
+                    help="batch-1 latency (BASELINE configs[1]): timed repeats after --latency-warmup (SURVEY §8d: 50 + 5)")
+    ap.add_argument("--latency-warmup", type=int, default=5)
+    ap.add_argument("--beam5-latency-repeats", type=int, default=20,
+                    help="batch-1 latency with the reference's beam_size=5 (after --latency-warmup)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--beam5", type=int, default=1, help="also time one isolated beam-5 step (the reference default)")
     ap.add_argument("--beam5-steps", type=int, default=3,
                     help="also time this many beam-5 steps on the lanes (after the greedy timed region)")
     ap.add_argument("--cpu-decode-steps", type=int, default=8)
+    ap.add_argument("--realistic-steps", type=int, default=6,
+                    help="also time this many steps with realistic output lengths (random weights never emit "
+                         "<|endoftext|>: each clip's length is forced from a seeded distribution)")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_v16_pmc.json"),
                     help="per-kernel HBM bytes from a rocprofv3 --pmc pass (tools/pmc_summary.py)")
     return ap.parse_args()
@@ -163,6 +170,37 @@ def main():
     value = audio_s / el
     tokens_per_clip = ntok / (n_total * a.steps)
 
+    # Realistic output lengths: real speech gives ~2-6 tokens per second of audio (text +
+    # timestamp pairs), so each clip's greedy decode is cut at a length drawn from
+    # N(130, 40) clipped to [16, 440] (seeded; the same lengths on every rank) by the
+    # decoder's token budget.  Finished rows skip their self / cross-attention, so a
+    # batch's cost follows its clips' lengths, not the longest one's worst case.
+    realistic = None
+    if a.realistic_steps > 0:
+        lens = np.clip(np.round(np.random.default_rng(77).normal(130, 40, B)), 16, 440).astype(int)
+        import dataclasses
+        dp.cfg = dataclasses.replace(cfg, token_budget=tuple(int(x) for x in lens))
+        dp.run_steps(allpcm, len(dp.lanes))
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        tr0 = time.perf_counter()
+        rres = dp.run_steps(allpcm, a.realistic_steps)
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        rel = time.perf_counter() - tr0
+        if dist:
+            t = torch.tensor([rel], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            rel = float(t.item())
+        rtok = sum(len(o.tokens) for outs, _ in rres for o in outs) / (B * a.realistic_steps)
+        realistic = {"value": round(n_total * a.realistic_steps * 30.0 / rel, 2), "unit": "audio-sec/sec",
+                     "steps": a.realistic_steps, "ms_per_step": round(rel / a.realistic_steps * 1e3, 2),
+                     "tokens_per_clip": round(rtok, 1), "max_tokens_per_clip": int(lens.max()),
+                     "lengths": "N(130, 40) clipped to [16, 440], seed 77"}
+        dp.cfg = cfg
+
     # The reference's own decoding (beam_size=5, src/backends/faster_whisper.py:237) on the
     # same lanes: warm-up steps let every lane capture its beam graph, then K_b timed steps.
     beam5_lanes = None
@@ -242,15 +280,28 @@ def main():
                                  offsets=np.arange(B + 1, dtype=np.int64) * allpcm.shape[-1])
             beam5 = round(B * 30.0 / (time.perf_counter() - tb), 2)
 
-        # p50 latency at batch 1 (BASELINE configs[1])
-        lat = []
+        # latency of one 30 s clip at batch 1 (BASELINE configs[1]): warm-ups, then timed repeats
         one = torch.from_numpy(make_clips(1, offset=999)).to(dev)
-        for _ in range(a.latency_repeats):
-            torch.cuda.synchronize(dev)
-            t1 = time.perf_counter()
-            eng.transcribe_batch(None, cfg, device_pcm=one.data_ptr(), offsets=np.array([0, 480000], np.int64))
-            lat.append((time.perf_counter() - t1) * 1e3)
-        p50 = float(np.median(lat)) if lat else None
+        offs1 = np.array([0, 480000], np.int64)
+
+        def latency(c, repeats):
+            for _ in range(a.latency_warmup if repeats else 0):
+                eng.transcribe_batch(None, c, device_pcm=one.data_ptr(), offsets=offs1)
+            lat = []
+            for _ in range(repeats):
+                torch.cuda.synchronize(dev)
+                t1 = time.perf_counter()
+                eng.transcribe_batch(None, c, device_pcm=one.data_ptr(), offsets=offs1)
+                lat.append((time.perf_counter() - t1) * 1e3)
+            if not lat:
+                return None
+            return {"p50_ms": round(float(np.median(lat)), 2), "p95_ms": round(float(np.percentile(lat, 95)), 2),
+                    "repeats": repeats, "warmup": a.latency_warmup}
+
+        lat_greedy = latency(cfg, a.latency_repeats)
+        lat_beam = latency(DecodeConfig(suppress_tokens=sup, max_length=a.max_length, beam_size=5),
+                           a.beam5_latency_repeats)
+        p50 = lat_greedy["p50_ms"] if lat_greedy else None
 
         cpu = None
         if not a.no_cpu_baseline and world == 1:
@@ -266,8 +317,10 @@ def main():
                        "clips_per_gpu": B, "global_batch": n_total, "parallelism": f"dp{world}",
                        "lanes_per_gpu": len(dp.lanes)},
             "tokens_per_clip": round(tokens_per_clip, 1),
-            "p50_latency_ms_b1": None if p50 is None else round(p50, 2),
+            "p50_latency_ms_b1": p50,
+            "latency_b1": {"greedy": lat_greedy, "beam5": lat_beam},
             "beam5": beam5_lanes,
+            "realistic_lengths": realistic,
             "beam5_audio_sec_per_sec_1lane": beam5,
             "realtime_factor": round(value, 1),
             "roofline": roof,

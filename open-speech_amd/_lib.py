@@ -35,7 +35,7 @@ class osw_decode_opts(C.Structure):
                 ("language_tokens", C.POINTER(C.c_int32)),
                 ("beam_size", C.c_int32), ("patience", C.c_float), ("length_penalty", C.c_float),
                 ("num_hypotheses", C.c_int32), ("temperature", C.c_float), ("best_of", C.c_int32),
-                ("seed", C.c_uint64)]
+                ("seed", C.c_uint64), ("token_budget", C.POINTER(C.c_int32))]
 
 
 class osw_window_result(C.Structure):

@@ -118,8 +118,8 @@ struct GemmArgs {
     // decoder activations as an fp16 pair a = hi + lo (hi = fp16(a), lo = fp16(a - hi)):
     // A_lo has A's row addressing; the kernels accumulate hi·W then lo·W into the same
     // fp32 accumulators, so the product carries ~22 bits of the fp32 activation.
-    // nullptr: A alone (fp16 activations).  Supported by the skinny, wide and 128-tile
-    // kernels (the decoder's); the encoder's 256-tile kernels ignore it (host-checked).
+    // nullptr: A alone (fp16 activations).  Supported by the skinny and wide kernels (the
+    // decoder's); launch_gemm routes every A_lo GEMM to them.
     const h16* A_lo;
 };
 

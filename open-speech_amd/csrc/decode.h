@@ -22,7 +22,10 @@ struct SelParams {
     int num_hyp, max_cand; // beam stop rule: num_hypotheses, round(beam * patience)
     float length_penalty;
     float inv_temp;        // sampling (temperature > 0): 1 / temperature, else 0
-    unsigned long long seed;
+    const unsigned long long* seed;  // device word: the draw seed (not in the graph key, so a new
+                                     // seed per call replays the captured decode graph)
+    const int* budget;     // per decoder row: force <|endoftext|> after this many sampled tokens (<= 0: none);
+                           // nullptr: no budgets (osw_decode_opts::token_budget, length-controlled benches)
 };
 
 // Per window in beam mode: finished-hypothesis bookkeeping (the best one's tokens

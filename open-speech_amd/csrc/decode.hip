@@ -194,7 +194,8 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
                                                             const float* __restrict__ bias, h16* __restrict__ kcache,
                                                             h16* __restrict__ vcache, const int* __restrict__ pos_ptr,
                                                             int H, int B, int ctx, h16* __restrict__ out,
-                                                            int64_t lo_off, const int* __restrict__ anc, int group) {
+                                                            int64_t lo_off, const int* __restrict__ anc, int group,
+                                                            const SelState* __restrict__ st) {
     __shared__ h16 q16[HD];
     int h, b;
     if (anc) {
@@ -210,6 +211,9 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
         h = blockIdx.x % H;
         b = blockIdx.x / H;
     }
+    // a finished row (its <|endoftext|> is chosen; graph replays keep stepping it until
+    // the whole batch is done) reads and writes nothing: its outputs are never used
+    if (st[b].done) return;
     const int D = H * HD;
     const int pos = min(*pos_ptr, ctx - 1);  // graph replays may run past max_length on finished windows
     h16* kc = kcache + ((int64_t)b * H + h) * ctx * HD;
@@ -274,7 +278,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
                                                               const h16* __restrict__ xk, const h16* __restrict__ xv,
                                                               int H, int W, int T, int beam, float* __restrict__ ws,
                                                               int* __restrict__ ticket, h16* __restrict__ out,
-                                                              int64_t lo_off) {
+                                                              int64_t lo_off, const SelState* __restrict__ st) {
     __shared__ float red[4][NB][HD];
     __shared__ __attribute__((aligned(16))) float pvs[NB > 1 ? 4 : 1][8][HD];  // beam rows' P·V reduction image
     __shared__ float rm[4][NB], rl[4][NB];
@@ -285,6 +289,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
     const int p = (bid & 7) + 8 * (bid >> 6);  // (window, head) pair; its 8 chunks share one XCD (bid % 8)
     if (p >= W * H) return;
     const int h = p % H, w = p / H;
+    // a window whose rows are all finished skips its 384 KB of K/V per head (the 8 chunk
+    // workgroups of a (window, head) read the same flags, so none of them takes a ticket)
+    {
+        bool all_done = true;
+        for (int k = 0; k < beam; ++k) all_done = all_done && st[w * beam + k].done;
+        if (all_done) return;
+    }
     const int D = H * HD;
     const int per = (T + XCH - 1) / XCH;
     const int k0 = chunk * per, nk = min(T, k0 + per) - k0;
@@ -666,6 +677,7 @@ __device__ __forceinline__ void select_partial_body(const float* __restrict__ lo
     const RowRules R = row_rules(P, s);
     float m_all = -INFINITY, s_all = 0.f, m_ts = -INFINITY, s_ts = 0.f;
     ArgMax a_all{-INFINITY, 0x7fffffff}, a_text{-INFINITY, 0x7fffffff}, a_ts{-INFINITY, 0x7fffffff};
+    const unsigned long long seed = P.inv_temp > 0.f ? *P.seed : 0ull;
     for (int v = lo + tid; v < hi; v += 256) {
         const float xv = x[v];
         if (mode == SEL_SOT) {
@@ -677,7 +689,7 @@ __device__ __forceinline__ void select_partial_body(const float* __restrict__ lo
         lse_add(m_all, s_all, xv);
         // sampling: a_all / a_ts pick the Gumbel-perturbed maximum; a_text stays the plain
         // maximum (the timestamp-mass rule compares against it)
-        const float key = P.inv_temp > 0.f ? xv * P.inv_temp + gumbel_noise(P.seed, b, step, v) : xv;
+        const float key = P.inv_temp > 0.f ? xv * P.inv_temp + gumbel_noise(seed, b, step, v) : xv;
         a_all = amax(a_all, ArgMax{key, v});
         if (v >= P.tb) {
             lse_add(m_ts, s_ts, xv);
@@ -774,8 +786,12 @@ __device__ __forceinline__ void select_final_row(const float* __restrict__ logit
     }
     // log-prob of the pick under the rule-masked, untempered distribution (what openai /
     // faster-whisper accumulate); sampling keys are perturbed, so read the logit back
-    const float lp =
+    float lp =
         (P.inv_temp > 0.f ? logits[(int64_t)b * P.V + next] : (next == r.i_all ? r.v_all : r.v_ts)) - lse;
+    if (P.budget && P.budget[b] > 0 && n >= P.budget[b]) {  // length control: the row ends here
+        next = P.eot;
+        lp = logits[(int64_t)b * P.V + P.eot] - lse_all;
+    }
     s.sum_lp += lp;
     if (next == P.eot) {
         s.done = 1;
@@ -1114,13 +1130,15 @@ int sel_parts_bytes() { return (int)sizeof(SelPart) * SEL_SPLIT; }
 int beam_cand_bytes(int beam) { return (int)sizeof(BeamCand) * BEAM_SLICES * 2 * beam; }
 
 void launch_dec_self_attn(const float* part, int ks, const float* bias, h16* kc, h16* vc, const int* pos, int B,
-                          int H, int ctx, h16* out, int64_t lo_off, const int* anc, int group, hipStream_t s) {
+                          int H, int ctx, h16* out, int64_t lo_off, const int* anc, int group, const SelState* st,
+                          hipStream_t s) {
     dec_self_attn_kernel<<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, lo_off, anc,
-                                               anc ? group : 1);
+                                               anc ? group : 1, st);
 }
 
 void launch_dec_cross_attn(const float* part, int ks, const float* bias, const h16* xk, const h16* xv, int B, int H,
-                           int T, int beam, h16* out, int64_t lo_off, float* ws, int* ticket, hipStream_t s) {
+                           int T, int beam, h16* out, int64_t lo_off, float* ws, int* ticket, const SelState* st,
+                           hipStream_t s) {
     static const bool legacy = std::getenv("OSW_XATTN_LEGACY") != nullptr;  // A/B switch: one workgroup per (row, head)
     if (legacy || !ws) {
         dec_cross_attn_kernel<<<H * B, 256, 0, s>>>(part, ks, bias, xk, xv, H, B, T, beam, out, lo_off);
@@ -1129,12 +1147,12 @@ void launch_dec_cross_attn(const float* part, int ks, const float* bias, const h
     const int W = B / beam;
     const unsigned grid = (unsigned)(((W * H + 7) / 8) * 8 * XCH);
     switch (beam) {
-        case 1: dec_xattn_chunk_kernel<1><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off); break;
-        case 2: dec_xattn_chunk_kernel<2><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off); break;
+        case 1: dec_xattn_chunk_kernel<1><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off, st); break;
+        case 2: dec_xattn_chunk_kernel<2><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off, st); break;
         case 3:
-        case 4: dec_xattn_chunk_kernel<4><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off); break;
-        case 5: dec_xattn_chunk_kernel<5><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off); break;
-        default: dec_xattn_chunk_kernel<8><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off); break;
+        case 4: dec_xattn_chunk_kernel<4><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off, st); break;
+        case 5: dec_xattn_chunk_kernel<5><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off, st); break;
+        default: dec_xattn_chunk_kernel<8><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off, st); break;
     }
 }
 

@@ -56,19 +56,15 @@ __device__ __forceinline__ void store_one(const GemmArgs& g, int m, int n, float
     }
 }
 
-// LO (hi/lo activations, GemmArgs::A_lo; decoder beam rows > 64): a third LDS
-// image per stage and two MFMAs per fragment pair; 96 KiB -> one workgroup per CU.
-template <int EPI, bool LO = false>
-__global__ __launch_bounds__(NTHR, LO ? 1 : 2) void gemm_kernel(GemmArgs g) {
-    constexpr int NIMG = LO ? 3 : 2;  // [A | W | A_lo]
-    __shared__ __attribute__((aligned(16))) h16 lds[2][NIMG][BM * BK];  // [buf][A|W(|A_lo)], 64 / 96 KiB
+template <int EPI>
+__global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
+    __shared__ __attribute__((aligned(16))) h16 lds[2][2][BM * BK];  // [buf][A|W], 64 KiB
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
     const int kc = g.kc > 0 ? g.kc : g.K, kbeg = blockIdx.z * kc;  // split-K: slab blockIdx.z
 
     // per-thread source rows for the 4 A and 4 W glds pieces (fixed over K)
     const h16* asrc[4];
-    const h16* lsrc[LO ? 4 : 1];
     const h16* wsrc[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -77,7 +73,6 @@ __global__ __launch_bounds__(NTHR, LO ? 1 : 2) void gemm_kernel(GemmArgs g) {
         const int gm = min(m0 + r, g.M - 1);
         const int gn = min(n0 + r, g.N - 1);
         asrc[i] = grp_row(g.A, gm, g.a_grp_rows, g.a_grp_stride, g.lda) + c * 8 + kbeg;
-        if constexpr (LO) lsrc[i] = grp_row(g.A_lo, gm, g.a_grp_rows, g.a_grp_stride, g.lda) + c * 8 + kbeg;
         wsrc[i] = g.W + (int64_t)gn * g.ldw + c * 8 + kbeg;
     }
 
@@ -88,9 +83,6 @@ __global__ __launch_bounds__(NTHR, LO ? 1 : 2) void gemm_kernel(GemmArgs g) {
             h16* dw = &lds[buf][1][(i * 4 + wave) * 8 * BK];
             __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + k0), (OSW_LDS void*)da, 16, 0, 0);
             __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + k0), (OSW_LDS void*)dw, 16, 0, 0);
-            if constexpr (LO)
-                __builtin_amdgcn_global_load_lds((const void*)(lsrc[i] + k0),
-                                                 (OSW_LDS void*)&lds[buf][NIMG - 1][(i * 4 + wave) * 8 * BK], 16, 0, 0);
         }
     };
 
@@ -110,16 +102,14 @@ __global__ __launch_bounds__(NTHR, LO ? 1 : 2) void gemm_kernel(GemmArgs g) {
         if (kt + 1 < nk) stage(buf ^ 1, (kt + 1) * BK);
         const h16* la = lds[buf][0];
         const h16* lw = lds[buf][1];
-        const h16* ll = lds[buf][NIMG - 1];
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             const int c = ks * 4 + (lane >> 4);
-            h16x8 a[4], b[4], al[LO ? 4 : 1];
+            h16x8 a[4], b[4];
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi) {
                 const int row = wm * 64 + mi * 16 + (lane & 15);
                 a[mi] = *(const h16x8*)&la[row * BK + swz(row, c) * 8];
-                if constexpr (LO) al[mi] = *(const h16x8*)&ll[row * BK + swz(row, c) * 8];
             }
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni) {
@@ -129,11 +119,8 @@ __global__ __launch_bounds__(NTHR, LO ? 1 : 2) void gemm_kernel(GemmArgs g) {
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-                for (int ni = 0; ni < 4; ++ni) {
+                for (int ni = 0; ni < 4; ++ni)
                     acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
-                    if constexpr (LO)
-                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[mi], b[ni], acc[mi][ni], 0, 0, 0);
-                }
         }
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
@@ -711,24 +698,29 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
         }
 }
 
-// Wide-N, few-row GEMM (decoder logits: M <= 64 rows x 51866 vocabulary columns,
-// K = d_model): the weights (133 MB at turbo) are streamed once per step and the
-// few activation rows are re-read from L2.  Tile 64 rows x 128 columns, 4 waves of
-// 64 x 32; a 3-slot LDS ring keeps two 64-deep K tiles in flight per workgroup
-// (72 KB -> 2 workgroups per CU, so the 406 tiles of the vocabulary are resident at
-// once), where the generic 128x128 kernel keeps one and waits a full HBM round trip
-// per K tile.  fp32 out, written through L2 (device-scope stores) for the select
-// kernels.
+// Wide-N GEMM for the decoder (logits: 64-row tiles x the 51866 vocabulary columns;
+// beam search's > 64 rows: every projection): 64 rows x 128 columns per workgroup,
+// 4 waves of 64 x 32, fp32 out written through L2 (device-scope stores) for the
+// consumer kernels.  A 3-slot LDS ring keeps two 64-deep weight tiles in flight
+// per workgroup (the generic 128x128 kernel keeps one and waits a full HBM round
+// trip per K tile: 44.9 -> 35.8 us per logits step at 64 rows).  Grid: x = column
+// tiles, y = 64-row tiles, z = split-K slabs (g.kc > 0: slab z at C + z*M*ldc, no
+// bias, the projections of beam rows).
+// LO (hi/lo activations, GemmArgs::A_lo): the activations come from L2 (tiny, hot),
+// so their ring is only 2 slots, staged one tile ahead instead of two: 32 KB of A
+// (hi + lo) + 48 KB of W = 80 KB, 2 workgroups per CU as without LO (the 96 KB
+// 3-slot version held one per CU and ran the 406 logits tiles in two rounds:
+// 58.8 us per step).
 constexpr int WBM = 64, WBN = 128, WSL = 3;
-// LO (hi/lo activations, GemmArgs::A_lo): a second A ring image and two MFMAs per
-// fragment pair; 96 KB of LDS -> one workgroup per CU.
 template <bool LO>
-__global__ __launch_bounds__(256, LO ? 1 : 2) void gemm_wide_kernel(GemmArgs g) {
+__global__ __launch_bounds__(256, 2) void gemm_wide_kernel(GemmArgs g) {
     constexpr int NIMG = LO ? 2 : 1;
-    __shared__ __attribute__((aligned(16))) h16 la[WSL][NIMG][WBM * BK];
+    constexpr int ASL = LO ? 2 : WSL;  // A ring slots
+    __shared__ __attribute__((aligned(16))) h16 la[ASL][NIMG][WBM * BK];
     __shared__ __attribute__((aligned(16))) h16 lw[WSL][WBN * BK];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int n0 = blockIdx.x * WBN;
+    const int n0 = blockIdx.x * WBN, m0 = blockIdx.y * WBM;
+    const int kc = g.kc > 0 ? g.kc : g.K, kbeg = blockIdx.z * kc;
     // staging: one wave-instruction fills 8 rows x 64 k (1 KiB); A 8 groups (2 per
     // wave) per image, W 16 groups (4 per wave); the 16-B chunk is XOR-swizzled by row
     const h16* asrc[NIMG][2];
@@ -736,21 +728,24 @@ __global__ __launch_bounds__(256, LO ? 1 : 2) void gemm_wide_kernel(GemmArgs g) 
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int r = (i * 4 + wave) * 8 + (lane >> 3);
-        asrc[0][i] = g.A + (int64_t)min(r, g.M - 1) * g.lda + swz(r, lane & 7) * 8;
-        if constexpr (LO) asrc[NIMG - 1][i] = g.A_lo + (int64_t)min(r, g.M - 1) * g.lda + swz(r, lane & 7) * 8;
+        const int64_t gm = min(m0 + r, g.M - 1);
+        asrc[0][i] = g.A + gm * g.lda + swz(r, lane & 7) * 8 + kbeg;
+        if constexpr (LO) asrc[NIMG - 1][i] = g.A_lo + gm * g.lda + swz(r, lane & 7) * 8 + kbeg;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int r = (i * 4 + wave) * 8 + (lane >> 3);
-        wsrc[i] = g.W + (int64_t)min(n0 + r, g.N - 1) * g.ldw + swz(r, lane & 7) * 8;
+        wsrc[i] = g.W + (int64_t)min(n0 + r, g.N - 1) * g.ldw + swz(r, lane & 7) * 8 + kbeg;
     }
-    auto stage = [&](int slot, int k0) {
+    auto stageA = [&](int slot, int k0) {
 #pragma unroll
         for (int im = 0; im < NIMG; ++im)
 #pragma unroll
             for (int i = 0; i < 2; ++i)
                 __builtin_amdgcn_global_load_lds((const void*)(asrc[im][i] + k0),
                                                  (OSW_LDS void*)&la[slot][im][(i * 4 + wave) * 8 * BK], 16, 0, 0);
+    };
+    auto stageW = [&](int slot, int k0) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + k0), (OSW_LDS void*)&lw[slot][(i * 4 + wave) * 8 * BK],
@@ -761,18 +756,33 @@ __global__ __launch_bounds__(256, LO ? 1 : 2) void gemm_wide_kernel(GemmArgs g) 
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int nk = g.K / BK;
-    stage(0, 0);
-    if (nk > 1) stage(1, BK);
+    const int nk = kc / BK;
+    // issue order per thread: A(0) W(0) W(1) | per iteration kt: A(kt+1) W(kt+2)
+    // (without LO, A(kt+2) rides with W(kt+2) as in the plain 3-slot ring)
+    if constexpr (LO) {
+        stageA(0, 0);
+        stageW(0, 0);
+        if (nk > 1) stageW(1, BK);
+    } else {
+        stageA(0, 0);
+        stageW(0, 0);
+        if (nk > 1) { stageA(1, BK); stageW(1, BK); }
+    }
     for (int kt = 0; kt < nk; ++kt) {
+        // tile kt has landed: younger than it are only tile kt+1's W (LO) or A+W
         if (kt + 1 < nk)
-            wait_vmcnt<2 * NIMG + 4>();  // this thread's tile kt has landed; tile kt+1 stays in flight
+            wait_vmcnt<LO ? 4 : 6>();
         else
             wait_vmcnt<0>();
-        __syncthreads();  // every thread's tile kt has landed; slot (kt+2)%3 is no longer read
-        if (kt + 2 < nk) stage((kt + 2) % WSL, (kt + 2) * BK);
-        const int sl = kt % WSL;
-        const h16* W = lw[sl];
+        __syncthreads();  // every thread's tile kt has landed; the slots refilled below are no longer read
+        if constexpr (LO) {
+            if (kt + 1 < nk) stageA((kt + 1) % ASL, (kt + 1) * BK);
+            if (kt + 2 < nk) stageW((kt + 2) % WSL, (kt + 2) * BK);
+        } else {
+            if (kt + 2 < nk) { stageA((kt + 2) % WSL, (kt + 2) * BK); stageW((kt + 2) % WSL, (kt + 2) * BK); }
+        }
+        const int sa = kt % ASL;
+        const h16* W = lw[kt % WSL];
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             const int c = ks * 4 + (lane >> 4);
@@ -782,7 +792,7 @@ __global__ __launch_bounds__(256, LO ? 1 : 2) void gemm_wide_kernel(GemmArgs g) 
 #pragma unroll
                 for (int mi = 0; mi < 4; ++mi) {
                     const int row = mi * 16 + (lane & 15);
-                    a[im][mi] = *(const h16x8*)&la[sl][im][row * BK + swz(row, c) * 8];
+                    a[im][mi] = *(const h16x8*)&la[sa][im][row * BK + swz(row, c) * 8];
                 }
 #pragma unroll
             for (int ni = 0; ni < 2; ++ni) {
@@ -799,20 +809,28 @@ __global__ __launch_bounds__(256, LO ? 1 : 2) void gemm_wide_kernel(GemmArgs g) 
                 }
         }
     }
+    float* C = (float*)g.C + (g.kc > 0 ? (int64_t)blockIdx.z * g.M * g.ldc : 0);
+    const float* bias = g.kc > 0 ? nullptr : g.bias;
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int m = mi * 16 + (lane >> 4) * 4 + i;
+            const int m = m0 + mi * 16 + (lane >> 4) * 4 + i;
             if (m >= g.M) continue;
 #pragma unroll
             for (int ni = 0; ni < 2; ++ni) {
                 const int n = n0 + wave * 32 + ni * 16 + (lane & 15);
                 if (n >= g.N) continue;
-                const float v = g.bias ? acc[mi][ni][i] + g.bias[n] : acc[mi][ni][i];
-                __hip_atomic_store((float*)g.C + (int64_t)m * g.ldc + n, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const float v = bias ? acc[mi][ni][i] + bias[n] : acc[mi][ni][i];
+                __hip_atomic_store(C + (int64_t)m * g.ldc + n, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
+}
+
+void launch_wide(const GemmArgs& g, int ks, hipStream_t s) {
+    const dim3 grid((g.N + WBN - 1) / WBN, (g.M + WBM - 1) / WBM, ks);
+    if (g.A_lo) gemm_wide_kernel<true><<<grid, 256, 0, s>>>(g);
+    else gemm_wide_kernel<false><<<grid, 256, 0, s>>>(g);
 }
 
 template <int EPI>
@@ -886,17 +904,18 @@ int launch_gemm_skinny_partial(const GemmArgs& g, float* part, hipStream_t s) {
     return ks;
 }
 
-// Mid-size M (beam-search decoder rows, 65..~640): 128x128 tiles split over K so
-// the grid still fills the chip; each split writes its own fp32 slab, reduced by
-// the consumer kernel exactly like the skinny kernel's slabs.  Picks the largest
-// split (K/ks a multiple of 256... or 64) that keeps the grid near 512 workgroups.
+// Mid-size M (beam-search decoder rows, 65..~640): the wide kernel's 64x128 tiles split
+// over K so the grid still fills the chip; each split writes its own fp32 slab, reduced
+// by the consumer kernel exactly like the skinny kernel's slabs.  Picks the largest
+// split (K/ks a multiple of 64, >= 256 deep) that keeps the grid near 1024 workgroups
+// (2 per CU).
 int tiled_ksplit(int M, int N, int K) {
-    const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    const int tiles = ((M + WBM - 1) / WBM) * ((N + WBN - 1) / WBN);
     int best = 1;
     for (int ks = 1; ks <= K / BK; ++ks) {
         if (K % ks || (K / ks) % BK) continue;
         if ((K / ks) < 256 && ks > 1) break;
-        if (tiles * ks > 640) break;
+        if (tiles * ks > 1280) break;
         best = ks;
     }
     return best;
@@ -909,9 +928,7 @@ void launch_gemm_tiled_partial(const GemmArgs& g0, float* part, int ks, hipStrea
     g.ldc = g.N;
     g.bias = nullptr;
     g.epi = EPI_F32;
-    dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, ks);
-    if (g.A_lo) gemm_kernel<EPI_F32, true><<<grid, NTHR, 0, s>>>(g);
-    else gemm_kernel<EPI_F32><<<grid, NTHR, 0, s>>>(g);
+    launch_wide(g, ks, s);
 }
 
 void launch_gemm_skinny(const GemmArgs& g, float* part, hipStream_t s) {
@@ -930,23 +947,20 @@ void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s);
 void launch_gemm(const GemmArgs& g, hipStream_t s) { launch_gemm_variant(g, 0, s); }
 
 void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s) {
-    // few rows, very wide N, plain fp32 out (decoder logits): the 3-slot ring kernel
+    // few rows, very wide N, plain fp32 out (decoder logits): the 3-slot ring kernel; with
+    // hi/lo activations (the decoder) at any row count
     static const bool no_wide = getenv("OSW_NO_WIDE") != nullptr;  // A/B switch
-    const bool wide_ok = g.M <= WBM && g.epi == EPI_F32 && g.kc == 0 && g.c_grp_rows == g.M && g.K % BK == 0;
-    if (wide_ok && (variant == 5 || (variant == 0 && g.N >= 16384 && !no_wide))) {
-        if (g.A_lo) gemm_wide_kernel<true><<<(g.N + WBN - 1) / WBN, 256, 0, s>>>(g);
-        else gemm_wide_kernel<false><<<(g.N + WBN - 1) / WBN, 256, 0, s>>>(g);
+    const bool wide_ok = g.epi == EPI_F32 && g.kc == 0 && g.c_grp_rows == g.M && g.K % BK == 0 &&
+                         (g.M <= WBM || g.A_lo);
+    if (wide_ok && (variant == 5 || (variant == 0 && (g.A_lo || (g.N >= 16384 && !no_wide))))) {
+        launch_wide(g, 1, s);
         return;
     }
     // big tile when it still yields >= 2 waves of workgroups over 256 CUs
     const int64_t big_tiles = (int64_t)((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
     const bool big = !g.A_lo && (variant == 2 || (variant == 0 && big_tiles >= 512 && g.N % 8 == 0 &&
                                                    !getenv("OSW_GEMM128")));
-    if (g.A_lo && g.epi == EPI_F32) {  // decoder (hi/lo activations): the 128-tile kernel, fp32 logits
-        dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
-        gemm_kernel<EPI_F32, true><<<grid, NTHR, 0, s>>>(g);
-        return;
-    }
+
     static const bool two_phase = getenv("OSW_GEMM_2PHASE") != nullptr;  // A/B switch for the 8-phase schedule
     if (variant == 4 || (variant == 0 && big && !two_phase)) {
         switch (g.epi) {

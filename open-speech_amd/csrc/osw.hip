@@ -34,9 +34,9 @@ void launch_init_uniform(void*, bool, int64_t, uint64_t, float, float, int64_t, 
 uint64_t hash_stream_key(uint64_t, int64_t);
 void launch_dec_embed(const h16*, const float*, const int*, const int*, int, int, int, float*, hipStream_t);
 void launch_dec_self_attn(const float*, int, const float*, h16*, h16*, const int*, int, int, int, h16*, int64_t,
-                          const int*, int, hipStream_t);
+                          const int*, int, const SelState*, hipStream_t);
 void launch_dec_cross_attn(const float*, int, const float*, const h16*, const h16*, int, int, int, int, h16*, int64_t,
-                           float*, int*, hipStream_t);
+                           float*, int*, const SelState*, hipStream_t);
 void launch_dec_resid_ln(const float*, int, int, int, const float*, float*, const float*, const float*, h16*, int64_t,
                          const h16*, const float*, const int*, const int*, int, hipStream_t);
 void launch_dec_reduce_gelu(const float*, int, int, int, const float*, h16*, int64_t, hipStream_t);
@@ -167,6 +167,8 @@ struct osw_ctx {
     float* xws = nullptr;      // cross-attention per-chunk partials [R][H][XCHUNKS][XPART]
     int* xticket = nullptr;    // cross-attention arrival tickets [B][H] (zero between launches)
     int* sel_arrive = nullptr; // select arrival counters: rows finalised + per-row slice tickets (zero between launches)
+    int* budget = nullptr;     // per-row token budgets (osw_decode_opts::token_budget)
+    unsigned long long* seed_d = nullptr;  // sampling seed of the current decode call
     int64_t part_floats = 0;
 
     // decode-step graph (CH steps per replay), re-captured when its key changes
@@ -434,6 +436,8 @@ void setup_workspace(osw_ctx* c) {
     c->xws = dalloc<float>(R * d.n_text_head * XCHUNKS * XPART, o);
     c->xticket = dalloc<int>(B * d.n_text_head, o);
     HIPCHK(hipMemset(c->xticket, 0, (size_t)B * d.n_text_head * sizeof(int)));
+    c->budget = dalloc<int>(R, o);
+    c->seed_d = dalloc<unsigned long long>(1, o);
     c->sel_arrive = dalloc<int>(1 + R, o);  // [0] rows finalised, [1 + row] slice tickets
     HIPCHK(hipMemset(c->sel_arrive, 0, (1 + (size_t)R) * sizeof(int)));
     {
@@ -597,7 +601,7 @@ void decoder_step(osw_ctx* c, int nb, int group, bool gather) {
         const std::string p = "dec.l" + std::to_string(l);
         int ks = partial(c->xdn, D, WH(c, p + ".qkv.w"), 3 * D, D);
         launch_dec_self_attn(c->part, ks, WF(c, p + ".qkv.b"), c->kc + l * kv_layer, c->vc + l * kv_layer, c->pos, nb,
-                             H, ctx, c->dattn, lo_d, gather ? c->anc : nullptr, group, c->stream);
+                             H, ctx, c->dattn, lo_d, gather ? c->anc : nullptr, group, c->sel, c->stream);
         ks = partial(c->dattn, D, WH(c, p + ".o.w"), D, D);
         launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".o.b"), c->xd, WF(c, p + ".ln2.g"), WF(c, p + ".ln2.b"),
                             c->xdn, lo_d, nullptr, nullptr, nullptr, nullptr, ctx, c->stream);
@@ -606,7 +610,7 @@ void decoder_step(osw_ctx* c, int nb, int group, bool gather) {
             Timed t(c, CL_XATTN, 2.0 * nb * H * (double)T_ENC * 64 * 2);
             launch_dec_cross_attn(c->part, ks, WF(c, p + ".xq.b"), c->XKV + (2 * l) * xkv_which,
                                   c->XKV + (2 * l + 1) * xkv_which, nb, H, T_ENC, group, c->dattn, lo_d, c->xws,
-                                  c->xticket, c->stream);
+                                  c->xticket, c->sel, c->stream);
         }
         ks = partial(c->dattn, D, WH(c, p + ".xo.w"), D, D);
         launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".xo.b"), c->xd, WF(c, p + ".ln3.g"), WF(c, p + ".ln3.b"),
@@ -690,7 +694,16 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
     SP.max_cand = std::max(1, (int)std::lround(beam * (o->patience > 0.f ? o->patience : 1.f)));
     SP.length_penalty = o->length_penalty;
     SP.inv_temp = sampling ? 1.f / o->temperature : 0.f;
-    SP.seed = o->seed;
+    HIPCHK(hipMemcpyAsync(c->seed_d, &o->seed, 8, hipMemcpyHostToDevice, c->stream));
+    SP.seed = c->seed_d;
+    SP.budget = nullptr;
+    if (o->token_budget) {
+        REQUIRE(beam == 1, "token_budget applies to greedy and sampling decodes");
+        std::vector<int> bud(rows);
+        for (int i = 0; i < rows; ++i) bud[i] = o->token_budget[i / group];
+        HIPCHK(hipMemcpyAsync(c->budget, bud.data(), rows * 4, hipMemcpyHostToDevice, c->stream));
+        SP.budget = c->budget;
+    }
     auto select = [&] {
         launch_select(c->logits, rows, c->pos, SP, c->prompt, c->supmask, c->sel, c->cur_tok, c->tokens, max_tok,
                       c->selp, c->sel_arrive, beam == 1, c->stream);
@@ -711,7 +724,7 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
         std::vector<int64_t> key = {nb, P, n_pre, max_len, o->eot, o->no_speech, o->no_timestamps,
                                     o->timestamp_begin, o->blank, o->first_lang, o->n_langs, o->suppress_blank,
                                     o->without_timestamps, o->max_initial_timestamp_index, beam, SP.num_hyp,
-                                    SP.max_cand, lp_bits, group, it_bits, (int64_t)SP.seed};
+                                    SP.max_cand, lp_bits, group, it_bits, SP.budget ? 1 : 0};
         if (!c->dgraph || key != c->dgraph_key) {
             if (c->dgraph) {
                 HIPCHK(hipGraphExecDestroy(c->dgraph));

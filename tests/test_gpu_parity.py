@@ -354,3 +354,21 @@ def test_sampling_best_of_picks_best_row(tiny_engine):
     assert both[0].sum_logprob / max(1, len(both[0].tokens)) >= first.sum_logprob / max(1, len(first.tokens)) - 1e-6
     for o in both:
         assert np.isfinite(o.sum_logprob)
+
+
+def test_token_budget_and_finished_rows(tiny_engine):
+    """Length control: a window with a token budget ends after exactly that many tokens
+    (a prefix of its unlimited decode), and rows that finished early — whose self- and
+    cross-attention workgroups now return without reading their K/V — do not change the
+    other windows of the batch."""
+    d, eng, _ = tiny_engine
+    sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+    clips = [synth.chirp_clip(60 + i, 30.0) for i in range(4)]
+    free = eng.transcribe_batch(clips, DecodeConfig(suppress_tokens=sup, max_length=96))
+    budget = (5, 0, 17, 0)
+    cut = eng.transcribe_batch(clips, DecodeConfig(suppress_tokens=sup, max_length=96, token_budget=budget))
+    for i, b in enumerate(budget):
+        if b > 0:
+            assert cut[i].tokens == free[i].tokens[:b], i
+        else:
+            assert cut[i].tokens == free[i].tokens and cut[i].sum_logprob == free[i].sum_logprob, i

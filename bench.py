@@ -58,6 +58,10 @@ def parse():
     ap.add_argument("--beam5-steps", type=int, default=3,
                     help="also time this many beam-5 steps on the lanes (after the greedy timed region)")
     ap.add_argument("--cpu-decode-steps", type=int, default=8)
+    ap.add_argument("--stream-sessions", type=int, default=32,
+                    help="BASELINE configs[4]: concurrent /v1/audio/stream sessions simulated through the backend "
+                         "(0 = skip)")
+    ap.add_argument("--stream-speech-s", type=float, default=6.0, help="seconds of speech per streaming session")
     ap.add_argument("--realistic-steps", type=int, default=6,
                     help="also time this many steps with realistic output lengths (random weights never emit "
                          "<|endoftext|>: each clip's length is forced from a seeded distribution)")
@@ -115,6 +119,116 @@ def cpu_baseline(dims, n_tokens_per_clip: float, decode_steps: int) -> dict:
                       f"{3 + n_tokens_per_clip:.0f} decoder steps per clip (the GPU run's mean)"}
 
 
+def stream_sessions(n_sessions: int, speech_s: float, model: str = "random:large-v3-turbo") -> dict:
+    """BASELINE configs[4]: n concurrent streaming sessions against the drop-in backend,
+    following src/streaming.py's control flow with a scripted VAD (the reference's own
+    test stand-in, tests/test_streaming_session_runtime.py:53-58): 100 ms chunks arrive in
+    real time; while speech is active every chunk re-transcribes the whole utterance so
+    far (_transcribe_utterance, src/streaming.py:357-420: json, temperature 0, utterances
+    < 0.1 s skipped) and the session awaits the call before its next chunk; 300 ms of
+    silence finalises (_finalize_utterance :422-481).  Calls go through a 4-thread
+    executor like _streaming_executor (:50-52), so at most 4 are in flight and the
+    backend batches them across sessions.  Random weights never emit <|endoftext|>: the
+    backend cuts each window at 4 tokens per second of audio (STT_HIP_TOKENS_PER_SEC,
+    bench-only).  The reference's default beam_size 5 is used."""
+    import asyncio
+    from concurrent.futures import ThreadPoolExecutor
+
+    from open_speech_amd.audio import pcm_to_wav
+    from open_speech_amd.backend import HipWhisperBackend
+
+    os.environ.setdefault("STT_HIP_TOKENS_PER_SEC", "4")
+    be = HipWhisperBackend()
+    be.load_model(model)
+    ex = ThreadPoolExecutor(max_workers=4, thread_name_prefix="stream-transcribe")
+    chunk = 1600
+    silence_s, endpoint = 0.5, int(16000 * 300 / 1000)
+    lat, finals = [], []
+
+    async def session(i, t0):
+        loop = asyncio.get_running_loop()
+        pcm = synth.chirp_clip(500 + i, speech_s + silence_s).tobytes()
+        utter, active, silence = bytearray(), False, 0
+
+        async def call():
+            if len(utter) < 3200:
+                return
+            wav = pcm_to_wav(bytes(utter), 16000)
+            ts = time.perf_counter()
+            await loop.run_in_executor(ex, lambda: be.transcribe(audio=wav, model=model, language=None,
+                                                                 response_format="json", temperature=0.0))
+            lat.append(time.perf_counter() - ts)
+
+        n = len(pcm) // (2 * chunk)
+        for c in range(n):
+            await asyncio.sleep(max(0.0, t0 + (c + 1) * 0.1 - loop.time()))   # real-time arrival
+            data = pcm[c * 2 * chunk:(c + 1) * 2 * chunk]
+            if c * 0.1 < speech_s:                                            # scripted VAD: speech
+                if not active:
+                    active, utter = True, bytearray()
+                utter.extend(data)
+                await call()
+            elif active:
+                silence += chunk
+                utter.extend(data)
+                if silence >= endpoint:
+                    await call()
+                    finals.append(loop.time() - (t0 + n * 0.1))   # lag of the final transcript
+                    active, utter, silence = False, bytearray(), 0
+                else:
+                    await call()
+
+    async def main():
+        loop = asyncio.get_running_loop()
+        t0 = loop.time() + 0.2
+        await asyncio.gather(*[session(i, t0 + 1.0 * i / max(1, n_sessions)) for i in range(n_sessions)])
+
+    wall0 = time.perf_counter()
+    asyncio.run(main())
+    wall = time.perf_counter() - wall0
+    ex.shutdown(wait=True)
+    be.unload_model(model)
+    audio = n_sessions * (speech_s + silence_s)
+    return {"sessions": n_sessions, "speech_s_per_session": speech_s, "chunk_ms": 100, "executor_threads": 4,
+            "transcriptions": len(lat), "transcriptions_per_s": round(len(lat) / wall, 1),
+            "call_latency_p50_ms": round(1e3 * float(np.median(lat)), 1) if lat else None,
+            "call_latency_p95_ms": round(1e3 * float(np.percentile(lat, 95)), 1) if lat else None,
+            "final_transcript_lag_p50_s": round(float(np.median(finals)), 3) if finals else None,
+            "final_transcript_lag_max_s": round(float(np.max(finals)), 3) if finals else None,
+            "audio_seconds": audio, "wall_s": round(wall, 2),
+            "realtime_factor": round(audio / wall, 2),
+            "note": "scripted VAD (speech then 0.5 s silence), 4 tokens/s length control, beam 5, random weights"}
+
+
+def timed_steps(dp, allpcm, k: int, dist=None, dev=None):
+    """The bench contract's timed region: barrier + device sync on both sides of exactly
+    k steps, then the MAX of the elapsed time over ranks and the SUM of tokens decoded.
+    Returns (seconds, total tokens over all ranks, per-step results of this rank)."""
+    import torch
+
+    def sync():
+        if dev is not None and dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    if dist:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    res = dp.run_steps(allpcm, k)
+    sync()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    ntok = sum(len(o.tokens) for outs, _ in res for o in outs)
+    if dist:
+        t = torch.tensor([el, float(ntok)], dtype=torch.float64, device=dev)
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        el, ntok = float(mx[0].item()), int(t[1].item())
+    return el, ntok, res
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -147,24 +261,8 @@ def main():
 
     # warm-up: every lane captures its decode graph
     dp.run_steps(allpcm, max(a.warmup, len(dp.lanes)) if a.warmup > 0 else 0)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    res = dp.run_steps(allpcm, a.steps)
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    ntok = sum(len(o.tokens) for outs, _ in res for o in outs)
+    el, ntok, res = timed_steps(dp, allpcm, a.steps, dist, dev)
     profs = [e.profile() for e in dp.lanes]
-    if dist:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-        nt = torch.tensor([ntok], dtype=torch.float64, device=dev)
-        dist.all_reduce(nt)
-        ntok = int(nt.item())
 
     audio_s = n_total * a.steps * 30.0
     value = audio_s / el
@@ -181,20 +279,8 @@ def main():
         import dataclasses
         dp.cfg = dataclasses.replace(cfg, token_budget=tuple(int(x) for x in lens))
         dp.run_steps(allpcm, len(dp.lanes))
-        if dist:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        tr0 = time.perf_counter()
-        rres = dp.run_steps(allpcm, a.realistic_steps)
-        torch.cuda.synchronize(dev)
-        if dist:
-            dist.barrier()
-        rel = time.perf_counter() - tr0
-        if dist:
-            t = torch.tensor([rel], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            rel = float(t.item())
-        rtok = sum(len(o.tokens) for outs, _ in rres for o in outs) / (B * a.realistic_steps)
+        rel, rtok_all, _ = timed_steps(dp, allpcm, a.realistic_steps, dist, dev)
+        rtok = rtok_all / (n_total * a.realistic_steps)
         realistic = {"value": round(n_total * a.realistic_steps * 30.0 / rel, 2), "unit": "audio-sec/sec",
                      "steps": a.realistic_steps, "ms_per_step": round(rel / a.realistic_steps * 1e3, 2),
                      "tokens_per_clip": round(rtok, 1), "max_tokens_per_clip": int(lens.max()),
@@ -207,20 +293,8 @@ def main():
     if a.beam5_steps > 0:
         dp.cfg = DecodeConfig(suppress_tokens=sup, max_length=a.max_length, beam_size=5)
         dp.run_steps(allpcm, len(dp.lanes))
-        if dist:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        tb0 = time.perf_counter()
-        bres = dp.run_steps(allpcm, a.beam5_steps)
-        torch.cuda.synchronize(dev)
-        if dist:
-            dist.barrier()
-        bel = time.perf_counter() - tb0
-        if dist:
-            t = torch.tensor([bel], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            bel = float(t.item())
-        btok = sum(len(o.tokens) for outs, _ in bres for o in outs) / (B * a.beam5_steps)
+        bel, btok_all, _ = timed_steps(dp, allpcm, a.beam5_steps, dist, dev)
+        btok = btok_all / (n_total * a.beam5_steps)
         beam5_lanes = {"value": round(n_total * a.beam5_steps * 30.0 / bel, 2), "unit": "audio-sec/sec",
                        "steps": a.beam5_steps, "ms_per_step": round(bel / a.beam5_steps * 1e3, 2),
                        "lanes_per_gpu": len(dp.lanes), "tokens_per_clip": round(btok, 1)}
@@ -303,6 +377,10 @@ def main():
                            a.beam5_latency_repeats)
         p50 = lat_greedy["p50_ms"] if lat_greedy else None
 
+        stream = None
+        if a.stream_sessions > 0 and world == 1:
+            stream = stream_sessions(a.stream_sessions, a.stream_speech_s)
+
         cpu = None
         if not a.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(dims, tokens_per_clip, a.cpu_decode_steps)
@@ -321,6 +399,7 @@ def main():
             "latency_b1": {"greedy": lat_greedy, "beam5": lat_beam},
             "beam5": beam5_lanes,
             "realistic_lengths": realistic,
+            "streaming": stream,
             "beam5_audio_sec_per_sec_1lane": beam5,
             "realtime_factor": round(value, 1),
             "roofline": roof,

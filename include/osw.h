@@ -94,10 +94,11 @@ typedef struct osw_decode_opts {
     float temperature;
     int32_t best_of;             /* <= 0 -> 1; windows * best_of <= 5 * max_batch */
     uint64_t seed;               /* draw seed (counter-hash Gumbel-max, reproducible) */
-    /* length control (greedy / sampling; benches of realistic output lengths with random
-     * weights, which never emit <|endoftext|> on their own): n_windows ints, window i
-     * emits <|endoftext|> once it has sampled token_budget[i] tokens (<= 0: no limit).
-     * NULL: off.  Not a reference option. */
+    /* length control (benches of realistic output lengths with random weights, which
+     * never emit <|endoftext|> on their own): n_windows ints; greedy / sampling rows
+     * emit <|endoftext|> once they have sampled token_budget[i] tokens, beam search
+     * treats that step as the last one (<= 0: no limit).  NULL: off.  Not a reference
+     * option. */
     const int32_t* token_budget;
 } osw_decode_opts;
 

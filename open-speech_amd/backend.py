@@ -243,10 +243,12 @@ class HipWhisperBackend:
                        prompt: str | None = None) -> dict[str, Any]:
         m = self._ensure_model(model_id)
         pcm = decode_audio_bytes(audio)
+        tps = os.environ.get("STT_HIP_TOKENS_PER_SEC")  # bench-only length control (segments.py)
         opts = TranscribeOptions(task=task, language=language if (language and task == "transcribe") else None,
                                  initial_prompt=prompt or None, temperature=float(temperature or 0.0),
                                  beam_size=int(os.environ.get("STT_HIP_BEAM_SIZE", "5")),
-                                 best_of=int(os.environ.get("STT_HIP_BEST_OF", "5")))
+                                 best_of=int(os.environ.get("STT_HIP_BEST_OF", "5")),
+                                 tokens_per_second=float(tps) if tps else None)
         res = m.runner.transcribe(pcm, opts)
         return shape_response(task, res, response_format)
 

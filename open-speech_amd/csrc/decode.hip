@@ -292,9 +292,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
     // a window whose rows are all finished skips its 384 KB of K/V per head (the 8 chunk
     // workgroups of a (window, head) read the same flags, so none of them takes a ticket)
     {
-        bool all_done = true;
-        for (int k = 0; k < beam; ++k) all_done = all_done && st[w * beam + k].done;
-        if (all_done) return;
+        int done = 1;  // every flag loaded at once (no short-circuit chain of dependent loads)
+#pragma unroll
+        for (int k = 0; k < NB; ++k)
+            if (k < beam) done &= st[w * beam + k].done;
+        if (done) return;
     }
     const int D = H * HD;
     const int per = (T + XCH - 1) / XCH;
@@ -327,7 +329,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
             if (k >= beam) break;
             float r = bias[h * HD + lane];
             r += red[0][k][lane] + red[1][k][lane] + red[2][k][lane] + red[3][k][lane];
-            qsh[k][lane] = (float)(h16)r;  // fp16(q); the 1/sqrt(64) scale is applied in fp32 below
+            qsh[k][lane] = (float)(h16)r * 0.125f;
         }
     }
     __syncthreads();
@@ -337,15 +339,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
     for (int k = 0; k < NB; ++k) {
         mx[k] = -INFINITY;
         if (k >= beam) continue;
-        // beam rows (VALU-bound, §5.5): 4 v_dot2_f32_f16 per score on the unscaled fp16 q
-        // (exact: qsh holds fp16 values) instead of 8 conversions + 8 FMAs, then the
-        // 1/sqrt(64) scale in fp32 (exact, a power of two); one row: q * 0.125 in fp32
+        // beam rows (VALU-bound, §5.5): q/8 in fp16 and 4 v_dot2_f32_f16 per score instead
+        // of 8 conversions + 8 FMAs.  fp16(q)/8 is exact while |q| >= 2^-11 (q/8 stays a
+        // normal fp16); smaller elements lose low mantissa bits, an error below 2^-25
+        // absolute per product, far inside the fp32 sums' own rounding.  (Scaling the
+        // fp32 dot instead costs one more VALU op per score in this VALU-bound kernel:
+        // 122 -> 130 us per launch, measured.)
         float q[8];
         h16x2 q2[4];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) q[i] = qsh[k][8 * c + i] * 0.125f;
+        for (int i = 0; i < 8; ++i) q[i] = qsh[k][8 * c + i];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) q2[i] = h16x2{(h16)qsh[k][8 * c + 2 * i], (h16)qsh[k][8 * c + 2 * i + 1]};
+        for (int i = 0; i < 4; ++i) q2[i] = h16x2{(h16)q[2 * i], (h16)q[2 * i + 1]};
 #pragma unroll
         for (int u = 0; u < XU; ++u) {
             float d = 0.f;
@@ -353,7 +358,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
                     d = __builtin_amdgcn_fdot2(h16x2{kf[u][2 * i], kf[u][2 * i + 1]}, q2[i], d, false);
-                d *= 0.125f;
             } else {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) d = fmaf((float)kf[u][i], q[i], d);
@@ -1023,7 +1027,8 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
     }
     if (tid == 0) {
         BeamWin bw = bwin[w];
-        const bool is_last = P.prompt_len + n + 1 >= P.max_length;
+        // the last step: max_length, or (length control) the window's token budget
+        const bool is_last = P.prompt_len + n + 1 >= P.max_length || (P.budget && P.budget[r0] > 0 && n + 1 >= P.budget[r0]);
         int sec = K;
         bool top_fin = false;
         improved = 0;

@@ -171,9 +171,12 @@ struct osw_ctx {
     unsigned long long* seed_d = nullptr;  // sampling seed of the current decode call
     int64_t part_floats = 0;
 
-    // decode-step graph (CH steps per replay), re-captured when its key changes
+    // decode-step graphs (CH steps per replay), one per key (batch rows, prompt length,
+    // decode options); a small LRU so a serving mix of batch sizes replays instead of
+    // re-capturing (the streaming collator meets batches of 1..4 windows)
+    std::map<std::vector<int64_t>, std::pair<hipGraphExec_t, uint64_t>> dgraphs;
+    uint64_t dgraph_tick = 0;
     hipGraphExec_t dgraph = nullptr;
-    std::vector<int64_t> dgraph_key;
     bool capturing = false;
     bool prof_eager = false;  // profiling mode 2: decode steps launched eagerly so the per-kernel timers see them
     bool use_graph = true;
@@ -698,7 +701,6 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
     SP.seed = c->seed_d;
     SP.budget = nullptr;
     if (o->token_budget) {
-        REQUIRE(beam == 1, "token_budget applies to greedy and sampling decodes");
         std::vector<int> bud(rows);
         for (int i = 0; i < rows; ++i) bud[i] = o->token_budget[i / group];
         HIPCHK(hipMemcpyAsync(c->budget, bud.data(), rows * 4, hipMemcpyHostToDevice, c->stream));
@@ -725,11 +727,21 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
                                     o->timestamp_begin, o->blank, o->first_lang, o->n_langs, o->suppress_blank,
                                     o->without_timestamps, o->max_initial_timestamp_index, beam, SP.num_hyp,
                                     SP.max_cand, lp_bits, group, it_bits, SP.budget ? 1 : 0};
-        if (!c->dgraph || key != c->dgraph_key) {
-            if (c->dgraph) {
-                HIPCHK(hipGraphExecDestroy(c->dgraph));
-                c->dgraph = nullptr;
+        auto hit = c->dgraphs.find(key);
+        if (hit != c->dgraphs.end()) {
+            c->dgraph = hit->second.first;
+            hit->second.second = ++c->dgraph_tick;
+        } else {
+            constexpr size_t kMaxGraphs = 16;
+            if (c->dgraphs.size() >= kMaxGraphs) {  // evict the least recently used
+                auto lru = c->dgraphs.begin();
+                for (auto it = c->dgraphs.begin(); it != c->dgraphs.end(); ++it)
+                    if (it->second.second < lru->second.second) lru = it;
+                HIPCHK(hipStreamSynchronize(c->stream));
+                HIPCHK(hipGraphExecDestroy(lru->second.first));
+                c->dgraphs.erase(lru);
             }
+            c->dgraph = nullptr;
             HIPCHK(hipStreamSynchronize(c->stream));
             hipGraph_t gr = nullptr;
             c->capturing = true;
@@ -748,7 +760,7 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
             hipError_t e = hipGraphInstantiate(&c->dgraph, gr, nullptr, nullptr, 0);
             (void)hipGraphDestroy(gr);
             HIPCHK(e);
-            c->dgraph_key = key;
+            c->dgraphs[key] = {c->dgraph, ++c->dgraph_tick};
         }
     }
     int steps = 0;
@@ -1070,7 +1082,7 @@ int osw_destroy(osw_ctx* c) {
             HIPCHK(hipStreamSynchronize(c->stream));
             for (auto& e : c->evs) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
             for (auto e : c->ev_free) (void)hipEventDestroy(e);
-            if (c->dgraph) (void)hipGraphExecDestroy(c->dgraph);
+            for (auto& kv : c->dgraphs) (void)hipGraphExecDestroy(kv.second.first);
             for (void* p : c->owned) (void)hipFree(p);
             if (c->done_host) (void)hipHostFree(c->done_host);
             (void)hipStreamDestroy(c->stream);

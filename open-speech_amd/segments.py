@@ -52,11 +52,14 @@ class TranscribeOptions:
     best_of: int = 5               # faster-whisper default; used when temperature > 0
     prompt_reset_on_temperature: float = 0.5
     seed: int = 0
+    # bench-only length control (STT_HIP_TOKENS_PER_SEC): random weights never emit
+    # <|endoftext|>, so each window's decode is cut at ceil(rate * window seconds) + 2
+    tokens_per_second: float | None = None
 
     def key(self):
         return (self.task, self.language, self.initial_prompt, self.condition_on_previous_text,
                 self.without_timestamps, tuple(self.suppress_tokens), self.suppress_blank, self.beam_size,
-                self.patience, self.length_penalty, self.temperature, self.best_of)
+                self.patience, self.length_penalty, self.temperature, self.best_of, self.tokens_per_second)
 
 
 @dataclass
@@ -168,6 +171,9 @@ def transcribe_clips(engine, pcm_list: list, opts: TranscribeOptions, tok: Whisp
                                    max_initial_timestamp_index=max_init, beam_size=beam, patience=opts.patience,
                                    length_penalty=opts.length_penalty, temperature=opts.temperature,
                                    best_of=opts.best_of, seed=(opts.seed + 0x9E3779B1 * calls) & (2**64 - 1))
+                if opts.tokens_per_second:
+                    cfg.token_budget = tuple(int(np.ceil(opts.tokens_per_second * z * FRAME_SEC)) + 2
+                                             for _, _, z in wins)
                 calls += 1
                 prefixes = [p for _, p in chunk] if _plen else None
                 outs = engine.decode(len(chunk), cfg, prefix=prefixes, languages=langs)

@@ -105,3 +105,59 @@ def test_single_rank_lanes_run_steps():
     res = dp.run_steps(pcm, 5)
     dp.close()
     assert [g for _, g in res] == [[[0, 9, 45], [10, 19, 145]]] * 5
+
+
+class SleepyEngine(EchoEngine):
+    """Rank r takes (r + 1) * 40 ms per step and decodes r + 1 tokens per clip."""
+
+    def __init__(self, rank):
+        self.rank = rank
+
+    def transcribe_batch(self, clips, cfg, device_pcm=None, offsets=None):
+        import time
+        time.sleep(0.04 * (self.rank + 1))
+        return [_Out(list(range(self.rank + 1))) for _ in clips]
+
+    def sibling(self):
+        return SleepyEngine(self.rank)
+
+
+def _bench_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    import osw_path
+    osw_path.load()
+    import bench
+    from open_speech_amd.distributed import DataParallelTranscriber
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        B, S, k = 3, 100, 4
+        dp = DataParallelTranscriber(SleepyEngine(rank), None, dist=dist, clips_per_rank=B, n_samples=S, ctx=8)
+        allpcm = torch.zeros((world * B, S), dtype=torch.int16) if rank == 0 else None
+        el, ntok, res = bench.timed_steps(dp, allpcm, k, dist, torch.device("cpu"))
+        q.put((rank, el, ntok, len(res)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_accounting_gloo():
+    """bench.py's timed region over ranks: the time is the MAX over ranks (the slow rank
+    sets it) and tokens are summed over ranks, so `value` = all ranks' audio / that time."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, el0, n0, k0), (_, el1, n1, k1) = got
+    assert el0 == el1                      # every rank reports the same (max) time
+    assert el0 >= 4 * 0.04 * 2             # at least the slow rank's 4 steps x 80 ms
+    assert n0 == n1 == 4 * 3 * (1 + 2)     # tokens summed over both ranks
+    assert k0 == k1 == 4

@@ -7,6 +7,7 @@
 // workgroup per (b, h); K rows are read 128 B per lane (8 x 16 B), V in 1 KiB
 // contiguous wave-instructions (8 rows x 128 B), scores stay in LDS.
 #include "decode.h"
+#include "resln.h"
 
 #include <climits>
 #include <cstdio>
@@ -476,77 +477,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
     }
 }
 
-// grid B, 1024 threads: x[b] += bias + Σ split-K partials (residual stream, fp32),
-// then LayerNorm(x[b]) -> y[b] fp16 (the next projection's operand).  Each thread
-// owns <= 2 columns and keeps 4 slab loads in flight.  With part == nullptr it is
-// the embedding entry: x[b] = tok_emb[tok[b]] + pos_emb[pos].
-__global__ __launch_bounds__(1024) void dec_resid_ln_kernel(const float* __restrict__ part, int ks, int B, int D,
-                                                            const float* __restrict__ bias, float* __restrict__ x,
-                                                            const float* __restrict__ g, const float* __restrict__ be,
-                                                            h16* __restrict__ y, int64_t lo_off,
-                                                            const h16* __restrict__ tok_emb,
-                                                            const float* __restrict__ pos_emb,
-                                                            const int* __restrict__ tok,
-                                                            const int* __restrict__ pos_ptr, int ctx) {
-    __shared__ float red[16];
-    const int b = blockIdx.x, tid = threadIdx.x;
-    constexpr int PER = 2;  // D <= 2048
-    float v[PER];
-    float s = 0.f;
-    const int64_t slab = (int64_t)B * D, rb = (int64_t)b * D;
-    int t = 0, pos = 0;
-    if (!part) {
-        t = tok[b];
-        pos = min(*pos_ptr, ctx - 1);
-    }
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int c = tid + 1024 * i;
-        float a = 0.f;
-        if (c < D) {
-            if (part) {
-                float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-                int k = 0;
-                for (; k + 3 < ks; k += 4) {
-                    a0 += part[(k + 0) * slab + rb + c];
-                    a1 += part[(k + 1) * slab + rb + c];
-                    a2 += part[(k + 2) * slab + rb + c];
-                    a3 += part[(k + 3) * slab + rb + c];
-                }
-                for (; k < ks; ++k) a0 += part[k * slab + rb + c];
-                a = x[rb + c] + (bias ? bias[c] : 0.f) + ((a0 + a1) + (a2 + a3));
-            } else {
-                a = (float)tok_emb[(int64_t)t * D + c] + pos_emb[(int64_t)pos * D + c];
-            }
-            x[rb + c] = a;
-        }
-        v[i] = a;
-        s += a;
-    }
-    const float mean = block_reduce_sum(s, red) / D;
-    float q = 0.f;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int c = tid + 1024 * i;
-        if (c < D) q += (v[i] - mean) * (v[i] - mean);
-    }
-    const float rstd = rsqrtf(block_reduce_sum(q, red) / D + 1e-5f);
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int c = tid + 1024 * i;
-        if (c < D) split_h16((v[i] - mean) * rstd * g[c] + be[c], y, y + lo_off, rb + c);
-    }
+// grid B, 256 threads: x[b] += bias + Σ split-K partials (residual stream, fp32), then
+// LayerNorm(x[b]) -> y[b] as an fp16 pair (the next projection's operand); with
+// part == nullptr the embedding entry x[b] = tok_emb[tok[b]] + pos_emb[pos].  The
+// arithmetic is resln_rows (resln.h), shared with the fused GEMM prologue.
+__global__ __launch_bounds__(256) void dec_resid_ln_kernel(ResLnArgs A, h16* __restrict__ y, int64_t lo_off) {
+    __shared__ float red[2 * 4];
+    const int b = blockIdx.x;
+    resln_rows<1, 8>(A, b, 1, true, red,
+                  [&](int, int c, float v) { split_h16(v, y, y + lo_off, (int64_t)b * A.D + c); });
 }
 
-// fc1: h[b][n] = fp16(gelu(bias + Σ partials))
+// fc1: h[b][n] = fp16 pair of gelu(bias + Σ partials) (gelu_reduce_one, shared with the
+// fused fc2 prologue)
 __global__ __launch_bounds__(256) void dec_reduce_gelu_kernel(const float* __restrict__ part, int ks, int64_t total,
                                                               int N, const float* __restrict__ bias,
                                                               h16* __restrict__ y, int64_t lo_off) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        float v = bias[i % N];
-        for (int k = 0; k < ks; ++k) v += part[k * total + i];
-        split_h16(gelu_erf(v), y, y + lo_off, i);
-    }
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x)
+        split_h16(gelu_reduce_one(part, ks, total, bias, i, (int)(i % N)), y, y + lo_off, i);
 }
 
 // ---------------------------------------------------------------------------
@@ -1164,7 +1112,8 @@ void launch_dec_cross_attn(const float* part, int ks, const float* bias, const h
 void launch_dec_resid_ln(const float* part, int ks, int B, int D, const float* bias, float* x, const float* g,
                          const float* be, h16* y, int64_t lo_off, const h16* tok_emb, const float* pos_emb,
                          const int* tok, const int* pos, int ctx, hipStream_t s) {
-    dec_resid_ln_kernel<<<B, 1024, 0, s>>>(part, ks, B, D, bias, x, g, be, y, lo_off, tok_emb, pos_emb, tok, pos, ctx);
+    ResLnArgs A{part, ks, (int64_t)B * D, bias, x, x, g, be, tok_emb, pos_emb, tok, pos, ctx, D};
+    dec_resid_ln_kernel<<<B, 256, 0, s>>>(A, y, lo_off);
 }
 
 void launch_dec_reduce_gelu(const float* part, int ks, int B, int N, const float* bias, h16* y, int64_t lo_off,

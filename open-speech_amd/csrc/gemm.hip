@@ -15,6 +15,7 @@
 // im2col copy, and lets a batch of windows with padded per-window buffers be one
 // GEMM.  The C side has the same addressing.
 #include "common.h"
+#include "resln.h"
 
 #include <cstdlib>
 
@@ -567,8 +568,8 @@ __device__ __forceinline__ void wait_vmcnt() {
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <int MT, bool DIRECT, int EPI, bool LO>
-__global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, float* __restrict__ part) {
+template <int MT, bool DIRECT, int EPI, bool LO, int PRO = PRO_NONE>
+__global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, float* __restrict__ part, ProArgs pa) {
     // Workgroup = 64 columns x one kc-deep K range; wave = 16 columns.  The
     // activation rows (M <= 64) of each CKK-deep K chunk are staged ONCE per
     // workgroup into LDS by global_load_lds (row-XOR swizzle on the 16-B chunk ->
@@ -580,6 +581,12 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
     // LO: a second image holds the activations' lo halves (GemmArgs::A_lo); every
     // weight fragment feeds two MFMAs (hi, then lo) into one accumulator.  At > 32
     // rows the chunk is 128 k so both images still fit 64 KB (2 workgroups per CU).
+    // PRO (<= 8 rows, hi/lo): the activation rows are not loaded but built by the
+    // workgroup from the producer's split-K slabs (resln.h) into an LDS image Ap while
+    // the first weight chunk is in flight: residual+LayerNorm of the whole row (PRO_RESLN)
+    // or the GELU reduce of this workgroup's K range (PRO_GELU).  The MFMA order is the
+    // plain kernel's, so both paths give identical results.
+    static_assert(PRO == PRO_NONE || (MT == 1 && LO), "the prologue serves <= 8 hi/lo rows");
     constexpr int CK = (LO && MT > 2) ? 4 : 8;  // k32 steps per chunk
     constexpr int CKK = CK * 32;                 // k per chunk
     constexpr int CPR = CKK / 8;                 // 16-B pieces of one row per chunk
@@ -587,7 +594,9 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
     constexpr int ROWS = MT * 16;
     constexpr int NIMG = LO ? 2 : 1;
     constexpr int APIECES = ROWS / RPP / 4;      // glds per wave per image per chunk
-    __shared__ __attribute__((aligned(16))) h16 As[2][NIMG][ROWS * CKK];
+    __shared__ __attribute__((aligned(16))) h16 As[PRO ? 1 : 2][NIMG][PRO ? 8 : ROWS * CKK];
+    __shared__ __attribute__((aligned(16))) h16 Ap[PRO ? 2 : 1][PRO ? PRO_ROWS : 1][PRO ? PRO_STRIDE : 8];
+    __shared__ float pred[PRO ? 2 * PRO_ROWS * 4 : 1];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nb = blockIdx.x * 64 + wave * 16;
     const int ks = blockIdx.y;
@@ -610,6 +619,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
         if constexpr (LO) asrc[NIMG - 1][i] = grp_row(g.A_lo, gr, g.a_grp_rows, g.a_grp_stride, g.lda) + k0;
     }
     auto stageA = [&](int buf, int c) {
+        if constexpr (PRO != PRO_NONE) return;
         // a short last chunk is staged from kc-CKK so every load stays inside this K range;
         // with kc < CKK the unused tail is clamped to the range's last 16 B (values unused)
         const int kk = min(c * CKK, kc - CKK > 0 ? kc - CKK : 0);
@@ -626,7 +636,9 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
 #pragma unroll
         for (int u = 0; u < CK; ++u) {
             const int st = min(c * CK + u, nsteps - 1);
-            wf[u] = *(const h16x8*)(wrow + 32 * st);  // (nt loads measured 8.1 vs 7.2 us: the weights are re-read every step)
+            // (nt loads measured 8.1 vs 7.2 us on the projections: their weights are re-read
+            // every step; nt on the logits stream alone left the batch-1 p50 unchanged)
+            wf[u] = *(const h16x8*)(wrow + 32 * st);
         }
     };
     f32x4 acc[MT];
@@ -643,20 +655,54 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) {
                 const int row = mt * 16 + li;
-                const int ch = ((u + shift) * 4 + gq) ^ (row & 15);
-                const h16x8 af = *(const h16x8*)&As[buf][0][row * CKK + ch * 8];
-                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, wf[u], acc[mt], 0, 0, 0);
-                if constexpr (LO) {
-                    const h16x8 al = *(const h16x8*)&As[buf][NIMG - 1][row * CKK + ch * 8];
-                    acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, wf[u], acc[mt], 0, 0, 0);
+                h16x8 af, al;
+                if constexpr (PRO != PRO_NONE) {
+                    // image column of k = k0 + c*CKK + 32u + 8gq (the whole row for RESLN, the
+                    // workgroup's K range for GELU); rows past M repeat row M-1 (discarded)
+                    const int r = min(row, g.M - 1);
+                    const int kk = (PRO == PRO_RESLN ? k0 : 0) + c * CKK + u * 32 + gq * 8;
+                    af = *(const h16x8*)&Ap[0][r][kk];
+                    al = *(const h16x8*)&Ap[PRO ? 1 : 0][r][kk];
+                } else {
+                    const int ch = ((u + shift) * 4 + gq) ^ (row & 15);
+                    af = *(const h16x8*)&As[buf][0][row * CKK + ch * 8];
+                    if constexpr (LO) al = *(const h16x8*)&As[buf][NIMG - 1][row * CKK + ch * 8];
                 }
+                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, wf[u], acc[mt], 0, 0, 0);
+                if constexpr (LO) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, wf[u], acc[mt], 0, 0, 0);
             }
         }
     };
-    constexpr int INFLIGHT = CK + NIMG * APIECES;  // one chunk's loads per lane
+    constexpr int INFLIGHT = CK + (PRO ? 0 : NIMG * APIECES);  // one chunk's loads per lane
     h16x8 wa[CK], wb[CK];
     loadW(wa, 0);
     stageA(0, 0);
+    if constexpr (PRO == PRO_RESLN) {
+        // every workgroup normalises all rows (a few KB from L2); one stores x'
+        const bool wx = blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0;
+        auto put = [&](int r, int c, float y) {
+            const h16 h = (h16)y;
+            Ap[0][r][c] = h;
+            Ap[PRO ? 1 : 0][r][c] = (h16)(y - (float)h);
+        };
+        // all slab loads of the row in one round trip (24 covers fc2's 20 slabs)
+        if (pa.ln.ks <= 8) resln_rows<PRO_ROWS, 8>(pa.ln, 0, g.M, wx, pred, put);
+        else resln_rows<PRO_ROWS, 24>(pa.ln, 0, g.M, wx, pred, put);
+        __syncthreads();
+    } else if constexpr (PRO == PRO_GELU) {
+        const int64_t slab = (int64_t)g.M * g.K;
+#pragma unroll
+        for (int r = 0; r < PRO_ROWS; ++r) {
+            if (r >= g.M) break;
+            for (int j = threadIdx.x; j < kc; j += 256) {
+                const float y = gelu_reduce_one(pa.part, pa.ks, slab, pa.bias, (int64_t)r * g.K + k0 + j, k0 + j);
+                const h16 h = (h16)y;
+                Ap[0][r][j] = h;
+                Ap[PRO ? 1 : 0][r][j] = (h16)(y - (float)h);
+            }
+        }
+        __syncthreads();
+    }
     for (int c = 0; c < nch; c += 2) {
         if (c + 1 < nch) {
             loadW(wb, c + 1);
@@ -848,11 +894,11 @@ void skinny_dispatch(const GemmArgs& g, int ksplit, float* part, hipStream_t s) 
     const dim3 grid((g.N + 63) / 64, ksplit);
     const int kc = g.K / ksplit;
     if (ksplit == 1) {
-        if (g.A_lo) gemm_skinny_kernel<MT, true, EPI, true><<<grid, 256, 0, s>>>(g, kc, part);
-        else gemm_skinny_kernel<MT, true, EPI, false><<<grid, 256, 0, s>>>(g, kc, part);
+        if (g.A_lo) gemm_skinny_kernel<MT, true, EPI, true><<<grid, 256, 0, s>>>(g, kc, part, ProArgs{});
+        else gemm_skinny_kernel<MT, true, EPI, false><<<grid, 256, 0, s>>>(g, kc, part, ProArgs{});
     } else {
-        if (g.A_lo) gemm_skinny_kernel<MT, false, EPI, true><<<grid, 256, 0, s>>>(g, kc, part);
-        else gemm_skinny_kernel<MT, false, EPI, false><<<grid, 256, 0, s>>>(g, kc, part);
+        if (g.A_lo) gemm_skinny_kernel<MT, false, EPI, true><<<grid, 256, 0, s>>>(g, kc, part, ProArgs{});
+        else gemm_skinny_kernel<MT, false, EPI, false><<<grid, 256, 0, s>>>(g, kc, part, ProArgs{});
         const int64_t total = (int64_t)g.M * g.N;
         splitk_reduce_kernel<EPI><<<(unsigned)std::min<int64_t>((total + 255) / 256, 1024), 256, 0, s>>>(g, ksplit, part);
     }
@@ -891,8 +937,8 @@ int launch_gemm_skinny_partial(const GemmArgs& g, float* part, hipStream_t s) {
     const int kc = g.K / ks;
 #define OSW_SKINNY_PART(MT_)                                                                     \
     do {                                                                                         \
-        if (g.A_lo) gemm_skinny_kernel<MT_, false, EPI_F32, true><<<grid, 256, 0, s>>>(g, kc, part);  \
-        else gemm_skinny_kernel<MT_, false, EPI_F32, false><<<grid, 256, 0, s>>>(g, kc, part);       \
+        if (g.A_lo) gemm_skinny_kernel<MT_, false, EPI_F32, true><<<grid, 256, 0, s>>>(g, kc, part, ProArgs{}); \
+        else gemm_skinny_kernel<MT_, false, EPI_F32, false><<<grid, 256, 0, s>>>(g, kc, part, ProArgs{}); \
     } while (0)
     switch (std::min(g.M, 64) <= 16 ? 1 : std::min(g.M, 64) <= 32 ? 2 : std::min(g.M, 64) <= 48 ? 3 : 4) {
         case 1: OSW_SKINNY_PART(1); break;
@@ -909,6 +955,23 @@ int launch_gemm_skinny_partial(const GemmArgs& g, float* part, hipStream_t s) {
 // by the consumer kernel exactly like the skinny kernel's slabs.  Picks the largest
 // split (K/ks a multiple of 64, >= 256 deep) that keeps the grid near 1024 workgroups
 // (2 per CU).
+// Fused small-batch form (<= PRO_ROWS hi/lo rows): the operand is built by the prologue
+// (resln.h).  direct: one K range, EPI_F32 straight into g.C (the logits); otherwise the
+// split-K slabs into part, as launch_gemm_skinny_partial.  Returns ksplit.
+int launch_gemm_skinny_pro(const GemmArgs& g, int pro, const ProArgs& pa, bool direct, float* part, hipStream_t s) {
+    const int ks = direct ? 1 : skinny_ksplit(g.N, g.K);
+    const dim3 grid((g.N + 63) / 64, ks, 1);
+    const int kc = g.K / ks;
+    if (direct) {
+        if (pro == PRO_RESLN) gemm_skinny_kernel<1, true, EPI_F32, true, PRO_RESLN><<<grid, 256, 0, s>>>(g, kc, part, pa);
+        else gemm_skinny_kernel<1, true, EPI_F32, true, PRO_GELU><<<grid, 256, 0, s>>>(g, kc, part, pa);
+    } else {
+        if (pro == PRO_RESLN) gemm_skinny_kernel<1, false, EPI_F32, true, PRO_RESLN><<<grid, 256, 0, s>>>(g, kc, part, pa);
+        else gemm_skinny_kernel<1, false, EPI_F32, true, PRO_GELU><<<grid, 256, 0, s>>>(g, kc, part, pa);
+    }
+    return ks;
+}
+
 int tiled_ksplit(int M, int N, int K) {
     const int tiles = ((M + WBM - 1) / WBM) * ((N + WBN - 1) / WBN);
     int best = 1;

@@ -21,6 +21,7 @@
 #include "../../include/osw.h"
 #include "common.h"
 #include "decode.h"
+#include "resln.h"
 
 namespace osw {
 // launchers from the other translation units
@@ -152,6 +153,7 @@ struct osw_ctx {
     // decoder workspace.  xdn / dattn / dh (the GEMM operands) are hi/lo fp16 pairs:
     // the lo halves sit R rows after the hi halves (lo_off below)
     float* xd = nullptr;
+    float* xd2 = nullptr;      // second residual buffer of the fused small-batch step (ping-pong)
     h16 *xdn = nullptr, *dqkv = nullptr, *dattn = nullptr, *dq = nullptr, *dh = nullptr, *kc = nullptr, *vc = nullptr;
     float* logits = nullptr;
     int *cur_tok = nullptr, *pos = nullptr, *tokens = nullptr, *prompt = nullptr, *done = nullptr;
@@ -164,6 +166,7 @@ struct osw_ctx {
     void* bcand = nullptr;     // beam: [R][SEL_SPLIT][2*beam] candidates
     int* done_host = nullptr;  // pinned
     float* part = nullptr;     // split-K partial slabs of the decoder GEMMs
+    float* part2 = nullptr;    // second slab buffer of the fused small-batch step (<= PRO_ROWS rows)
     float* xws = nullptr;      // cross-attention per-chunk partials [R][H][XCHUNKS][XPART]
     int* xticket = nullptr;    // cross-attention arrival tickets [B][H] (zero between launches)
     int* sel_arrive = nullptr; // select arrival counters: rows finalised + per-row slice tickets (zero between launches)
@@ -415,6 +418,7 @@ void setup_workspace(osw_ctx* c) {
     c->XKV = dalloc<h16>((int64_t)d.n_text_layer * 2 * Me * Dd, o);
     const int64_t R = c->R;
     c->xd = dalloc<float>(R * Dd, o);
+    c->xd2 = dalloc<float>(std::min<int64_t>(R, PRO_ROWS) * Dd, o);
     c->xdn = dalloc<h16>(2 * R * Dd, o);
     c->dqkv = dalloc<h16>(R * 3 * Dd, o);
     c->dattn = dalloc<h16>(2 * R * Dd, o);
@@ -454,6 +458,10 @@ void setup_workspace(osw_ctx* c) {
                 c->part_floats = std::max<int64_t>(c->part_floats,
                                                    (int64_t)tiled_ksplit((int)R, (int)nk[0], (int)nk[1]) * R * nk[0]);
         c->part = dalloc<float>(c->part_floats, o);
+        int64_t p2 = 0;
+        for (auto& nk : shapes)
+            if (nk[0] != d.n_vocab) p2 = std::max<int64_t>(p2, (int64_t)skinny_ksplit((int)nk[0], (int)nk[1]) * nk[0]);
+        c->part2 = dalloc<float>(p2 * std::min<int64_t>(R, PRO_ROWS), o);
     }
     HIPCHK(hipHostMalloc((void**)&c->done_host, sizeof(int), 0));
 }
@@ -562,6 +570,75 @@ void encode(osw_ctx* c, const osw_window* wins, int n) {
 }
 
 // ---------------------------- decoder --------------------------------------
+// One decoder row (batch-1 latency; PRO_ROWS): the
+// residual+LayerNorm and GELU-reduce kernels are not launched; each runs as the prologue
+// of the projection that consumes it (gemm_skinny_kernel<.., PRO>, resln.h), and the
+// embedding is the prologue of layer 0's qkv: 51 -> 34 launches per step, 4 x [qkv,
+// self-attn, o, q, cross-attn, xo, fc1, fc2] + logits + select.  The residual stream
+// ping-pongs between xd and xd2 (every workgroup of a GEMM reads x, one writes x'), the
+// slabs between part and part2 (a GEMM's prologue reads its producer's slabs while its
+// epilogue writes its own).  Same arithmetic as decoder_step's separate kernels.
+void decoder_step_fused(osw_ctx* c, int nb, int group, bool gather) {
+    const osw_dims& d = c->d;
+    const int D = d.n_text_state, H = d.n_text_head, L = d.n_text_layer, ctx = d.n_text_ctx;
+    const int64_t xkv_which = (int64_t)(nb / group) * H * T_ENC * 64;
+    const int64_t kv_layer = (int64_t)nb * H * ctx * 64;
+    const int64_t lo_d = (int64_t)c->R * D;
+    float* xs[2] = {c->xd, c->xd2};
+    float* ps[2] = {c->part, c->part2};
+    int xi = 0, last = 1, ks = 0;  // residual buffer holding x; slab buffer of the last GEMM
+    auto gemm = [&](const h16* A, const h16* Wt, int N, int K) {
+        GemmArgs g = gemm_plain(A, D, Wt, nullptr, nb, N, K, nullptr, 0, EPI_F32);
+        g.A_lo = A ? A + lo_d : nullptr;
+        return g;
+    };
+    // residual + LayerNorm prologue over the last GEMM's slabs (bias = its bias); part ==
+    // nullptr: the embedding entry
+    auto resln = [&](const float* bias, const std::string& ln, bool embed) {
+        ProArgs pa{};
+        pa.ln = ResLnArgs{embed ? nullptr : ps[last], ks, (int64_t)nb * D, bias, xs[xi], xs[xi ^ 1],
+                          WF(c, ln + ".g"), WF(c, ln + ".b"), WH(c, "dec.tok"), WF(c, "dec.pos"), c->cur_tok, c->pos,
+                          ctx, D};
+        xi ^= 1;
+        return pa;
+    };
+    auto plain = [&](const h16* A, const std::string& w, int N, int K) {
+        ks = launch_gemm_skinny_partial(gemm(A, WH(c, w), N, K), ps[last ^ 1], c->stream);
+        last ^= 1;
+    };
+    auto fused = [&](int pro, const ProArgs& pa, const std::string& w, int N, int K) {
+        ks = launch_gemm_skinny_pro(gemm(nullptr, WH(c, w), N, K), pro, pa, false, ps[last ^ 1], c->stream);
+        last ^= 1;
+    };
+    for (int l = 0; l < L; ++l) {
+        const std::string p = "dec.l" + std::to_string(l), pp = "dec.l" + std::to_string(l - 1);
+        fused(PRO_RESLN, l == 0 ? resln(nullptr, p + ".ln1", true) : resln(WF(c, pp + ".fc2.b"), p + ".ln1", false),
+              p + ".qkv.w", 3 * D, D);
+        launch_dec_self_attn(ps[last], ks, WF(c, p + ".qkv.b"), c->kc + l * kv_layer, c->vc + l * kv_layer, c->pos,
+                             nb, H, ctx, c->dattn, lo_d, gather ? c->anc : nullptr, group, c->sel, c->stream);
+        plain(c->dattn, p + ".o.w", D, D);
+        fused(PRO_RESLN, resln(WF(c, p + ".o.b"), p + ".ln2", false), p + ".xq.w", D, D);
+        {
+            Timed t(c, CL_XATTN, 2.0 * nb * H * (double)T_ENC * 64 * 2);
+            launch_dec_cross_attn(ps[last], ks, WF(c, p + ".xq.b"), c->XKV + (2 * l) * xkv_which,
+                                  c->XKV + (2 * l + 1) * xkv_which, nb, H, T_ENC, group, c->dattn, lo_d, c->xws,
+                                  c->xticket, c->sel, c->stream);
+        }
+        plain(c->dattn, p + ".xo.w", D, D);
+        fused(PRO_RESLN, resln(WF(c, p + ".xo.b"), p + ".ln3", false), p + ".fc1.w", 4 * D, D);
+        ProArgs pg{};
+        pg.part = ps[last]; pg.ks = ks; pg.bias = WF(c, p + ".fc1.b");
+        fused(PRO_GELU, pg, p + ".fc2.w", D, 4 * D);
+    }
+    const std::string pl = "dec.l" + std::to_string(L - 1);
+    GemmArgs gl = gemm(nullptr, WH(c, "dec.tok"), d.n_vocab, D);
+    gl.C = c->logits;
+    gl.ldc = d.n_vocab;
+    launch_gemm_skinny_pro(gl, PRO_RESLN, resln(WF(c, pl + ".fc2.b"), "dec.lnpost", false), true, nullptr,
+                           c->stream);
+    HIPCHK(hipGetLastError());
+}
+
 // One decoder step for nb windows.  Every projection is a split-K skinny GEMM whose
 // partial slabs are reduced by the kernel that consumes them (self/cross attention
 // for q/k/v, residual+LayerNorm for the out-projections and fc2, GELU for fc1).
@@ -597,6 +674,11 @@ void decoder_step(osw_ctx* c, int nb, int group, bool gather) {
         REQUIRE((int64_t)skinny_ksplit(N, K) * nb * N <= c->part_floats, "split-K workspace too small");
         return launch_gemm_skinny_partial(g, c->part, c->stream);
     };
+    static const bool no_fuse = getenv("OSW_NO_FUSE") != nullptr;  // A/B switch
+    if (nb <= PRO_ROWS && !no_fuse) {
+        decoder_step_fused(c, nb, group, gather);
+        return;
+    }
     // x = tok_emb[tok] + pos_emb[pos]; xdn = LN1_0(x)
     launch_dec_resid_ln(nullptr, 0, nb, D, nullptr, c->xd, WF(c, "dec.l0.ln1.g"), WF(c, "dec.l0.ln1.b"), c->xdn, lo_d,
                         WH(c, "dec.tok"), WF(c, "dec.pos"), c->cur_tok, c->pos, ctx, c->stream);

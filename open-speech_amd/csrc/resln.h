@@ -1,0 +1,174 @@
+// Decoder residual update + LayerNorm, in the ONE formulation that both the standalone
+// kernel (decode.hip, dec_resid_ln_kernel) and the fused prologue of the small-batch
+// decoder GEMM (gemm.hip, gemm_skinny_kernel<.., PRO>) run, so a window's results do not
+// depend on which of the two paths its batch size selected (bit-identical by
+// construction; tests/test_gpu_parity.py::test_batch_equals_single).
+//
+// Per row r:  x' = x + bias + Σ_k part[k][r]   (or the embedding tok_emb[tok] + pos_emb[pos])
+//             y  = (x' - mean) * rstd * g + b   (two-pass variance, eps 1e-5, fp32)
+// 256 threads; thread t owns columns 4t..4t+3 (one 16-B piece) and 1024 + t (D <= 1280).
+// Every slab piece of a row is loaded before any is added (8 slabs per batch, clamped
+// addresses, the surplus added as exact zeros), so a row costs one memory round trip
+// per 8 slabs; the sums run in slab order, the thread's 5 columns in order, then
+// wave_sum, then the 4 wave partials in order.
+#pragma once
+#include "common.h"
+
+namespace osw {
+
+struct ResLnArgs {
+    const float* part;  // split-K slabs [ks][rows][D]; nullptr = embedding entry
+    int ks;
+    int64_t slab;       // floats per slab
+    const float* bias;  // may be nullptr
+    const float* x_in;  // residual stream [rows][D]
+    float* x_out;       // updated residual stream (may alias x_in in the standalone kernel)
+    const float* g;
+    const float* b;
+    const h16* tok_emb;  // embedding entry: x' = tok_emb[tok[r]] + pos_emb[min(*pos, ctx-1)]
+    const float* pos_emb;
+    const int* tok;
+    const int* pos;
+    int ctx;
+    int D;
+};
+
+// rows r0 .. r0+nr-1 (nr <= NR); emit(r, c, y) receives every LayerNorm output;
+// write_x: this workgroup stores x'.  red: LDS scratch of 2 * NR * 4 floats.  KB: slab
+// loads per batch (the sums do not depend on it: the padding adds exact zeros).
+template <int NR, int KB, class Emit>
+__device__ __forceinline__ void resln_rows(const ResLnArgs& A, int r0, int nr, bool write_x, float* red, Emit emit) {
+#pragma clang fp contract(off)
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int D = A.D;
+    const bool h4 = 4 * t < D, h1 = 1024 + t < D;
+    const int c4 = h4 ? 4 * t : 0, c1 = h1 ? 1024 + t : 0;  // clamped: every load stays in the row
+    float v[NR][5];
+    int pos = 0;
+    if (!A.part) pos = min(*A.pos, A.ctx - 1);
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) v[r][i] = 0.f;
+        if (r >= nr) continue;
+        const int64_t rb = (int64_t)(r0 + r) * D;
+        f32x4 a4;
+        float a1;
+        if (A.part) {
+            f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
+            float s1 = 0.f;
+            for (int k0 = 0; k0 < A.ks; k0 += KB) {
+                f32x4 p4[KB];
+                float p1[KB];
+#pragma unroll
+                for (int j = 0; j < KB; ++j) {
+                    const int64_t o = (int64_t)min(k0 + j, A.ks - 1) * A.slab + rb;
+                    p4[j] = *(const f32x4*)(A.part + o + c4);
+                    p1[j] = A.part[o + c1];
+                }
+#pragma unroll
+                for (int j = 0; j < KB; ++j) {
+                    const bool in = k0 + j < A.ks;
+                    s4 += in ? p4[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+                    s1 += in ? p1[j] : 0.f;
+                }
+            }
+            a4 = *(const f32x4*)(A.x_in + rb + c4);
+            a1 = A.x_in[rb + c1];
+            if (A.bias) {
+                a4 += *(const f32x4*)(A.bias + c4);
+                a1 += A.bias[c1];
+            }
+            a4 += s4;
+            a1 += s1;
+        } else {
+            const int tk = A.tok[r0 + r];
+            const h16x4 e4 = *(const h16x4*)(A.tok_emb + (int64_t)tk * D + c4);
+            const float* pe = A.pos_emb + (int64_t)pos * D;
+            a4 = f32x4{(float)e4[0], (float)e4[1], (float)e4[2], (float)e4[3]} + *(const f32x4*)(pe + c4);
+            a1 = (float)A.tok_emb[(int64_t)tk * D + c1] + pe[c1];
+        }
+        if (write_x) {
+            if (h4) *(f32x4*)(A.x_out + rb + c4) = a4;
+            if (h1) A.x_out[rb + c1] = a1;
+        }
+        if (h4) {
+            v[r][0] = a4[0];
+            v[r][1] = a4[1];
+            v[r][2] = a4[2];
+            v[r][3] = a4[3];
+        }
+        if (h1) v[r][4] = a1;
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) s += v[r][i];
+        s = wave_sum(s);
+        if (l == 0) red[r * 4 + w] = s;
+    }
+    __syncthreads();
+    float mean[NR], rstd[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        mean[r] = (((red[r * 4 + 0] + red[r * 4 + 1]) + red[r * 4 + 2]) + red[r * 4 + 3]) / D;
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+            if (i < 4 ? h4 : h1) {
+                const float d = v[r][i] - mean[r];
+                q = fmaf(d, d, q);
+            }
+        q = wave_sum(q);
+        if (l == 0) red[(NR + r) * 4 + w] = q;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const float q = (((red[(NR + r) * 4 + 0] + red[(NR + r) * 4 + 1]) + red[(NR + r) * 4 + 2]) +
+                         red[(NR + r) * 4 + 3]);
+        rstd[r] = rsqrtf(q / D + 1e-5f);
+    }
+    const f32x4 g4 = *(const f32x4*)(A.g + c4), b4 = *(const f32x4*)(A.b + c4);
+    const float g1 = A.g[c1], b1 = A.b[c1];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        if (r >= nr) break;
+        if (h4)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) emit(r, c4 + i, fmaf((v[r][i] - mean[r]) * rstd[r], g4[i], b4[i]));
+        if (h1) emit(r, c1, fmaf((v[r][4] - mean[r]) * rstd[r], g1, b1));
+    }
+}
+
+// Operand prologue of the small-batch decoder GEMM (gemm.hip): the workgroup builds its
+// activation rows itself instead of loading them, so the kernel that produced them
+// (residual+LayerNorm, GELU reduce) is not launched at all.
+enum Pro : int { PRO_NONE = 0, PRO_RESLN = 1, PRO_GELU = 2 };
+constexpr int PRO_ROWS = 1;      // rows the prologue serves: batch-1 latency (every workgroup
+                                 // re-reads all rows' slabs, so 5 beam rows were slower, measured)
+constexpr int PRO_STRIDE = 1288; // halfs per LDS image row (D <= 1280; +8 staggers the banks)
+struct ProArgs {
+    ResLnArgs ln;        // PRO_RESLN: LayerNorm(x') of every row, all D columns
+    const float* part;   // PRO_GELU: the fc1 slabs [ks][M][K], K = this GEMM's K
+    int ks;
+    const float* bias;
+};
+
+// fc1 -> fc2 operand: fp16 pair of gelu(bias + Σ_k part[k][r][n]), k in order (the order of
+// dec_reduce_gelu_kernel, which shares this function)
+__device__ __forceinline__ float gelu_reduce_one(const float* part, int ks, int64_t slab, const float* bias,
+                                                 int64_t i, int n) {
+    float v = bias[n];
+    for (int k0 = 0; k0 < ks; k0 += 8) {  // 8 slab loads in flight, then the adds in order
+        float p[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) p[j] = part[(int64_t)min(k0 + j, ks - 1) * slab + i];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v += k0 + j < ks ? p[j] : 0.f;
+    }
+    return gelu_erf(v);
+}
+
+}  // namespace osw

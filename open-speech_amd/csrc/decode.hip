@@ -274,6 +274,46 @@ __global__ __launch_bounds__(256) void dec_cross_attn_kernel(const float* __rest
 constexpr int XCH = XCHUNKS, XKEYS = 192, XU = XKEYS / 32;
 static_assert(XCH == 8, "the (window, head) -> XCD map assumes 8 chunks");
 
+// merge of a (window, head)'s chunk partials in fixed chunk order: out = Σ e^(m_s - M) acc_s /
+// Σ e^(m_s - M) l_s (device-scope loads: the other chunks' partials may come from another
+// XCD's writes); beam rows are spread over the 4 waves so their load round trips overlap
+__device__ __forceinline__ void xattn_merge(const float* __restrict__ ws, int r0, int beam, int H, int h,
+                                            h16* __restrict__ out, int64_t lo_off) {
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, D = H * HD;
+    for (int k = wv; k < beam; k += 4) {
+        const float* src = ws + ((int64_t)(r0 + k) * H + h) * XCH * XPART;
+        float mm[XCH];
+        float M = -INFINITY;
+#pragma unroll
+        for (int q = 0; q < XCH; ++q) {
+            mm[q] = __hip_atomic_load(src + q * XPART, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            M = fmaxf(M, mm[q]);
+        }
+        float L = 0.f, O = 0.f;
+#pragma unroll
+        for (int q = 0; q < XCH; ++q) {
+            const float e = __expf(mm[q] - M);
+            L = fmaf(__hip_atomic_load(src + q * XPART + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), e, L);
+            O = fmaf(__hip_atomic_load(src + q * XPART + 4 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), e, O);
+        }
+        split_h16(O / L, out, out + lo_off, (int64_t)(r0 + k) * D + h * HD + lane);
+    }
+}
+
+// LDS writes of every wave visible, without draining the wave's outstanding global loads
+// (__syncthreads waits for vmcnt(0) too)
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+typedef __fp16 fp16x4_t __attribute__((__vector_size__(4 * sizeof(__fp16))));
+__device__ __forceinline__ h16x4 ds_read_tr(const h16* p) {  // ds_read_b64_tr_b16 (as attn.hip)
+    fp16x4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4f16((OSW_LDS fp16x4_t*)p);
+    return __builtin_bit_cast(h16x4, v);
+}
+
 template <int NB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 : NB > 1 ? 5 : 1))) void dec_xattn_chunk_kernel(const float* __restrict__ part, int ks,
                                                               const float* __restrict__ bias,
@@ -455,27 +495,202 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
     if (NB == 1 && wv != 0) return;  // one row: wave 0 merges alone
     __syncthreads();
     if (!last) return;
-    // merge in fixed chunk order: out = Σ e^(m_s - M) acc_s / Σ e^(m_s - M) l_s (device-scope
-    // loads: the other chunks' partials may come from another XCD's writes); beam rows
-    // are spread over the 4 waves so their load round trips overlap
-    for (int k = wv; k < beam; k += 4) {
-        const float* src = ws + ((int64_t)(r0 + k) * H + h) * XCH * XPART;
-        float mm[XCH];
-        float M = -INFINITY;
+    xattn_merge(ws, r0, beam, H, h, out, lo_off);
+}
+
+// Beam rows (2..8 per window): dec_xattn_chunk_kernel's (window, head, key chunk)
+// decomposition, partials and last-arriver merge, with the scores and P·V on MFMA (the
+// VALU form ran VALU-bound: 120 us per launch at 64 windows x 5 beams against 84 us for
+// the greedy rows' identical K/V bytes).  The window's rows are the 16 MFMA columns
+// (rows >= beam: q = 0, results unused).
+//   Sᵀ = K·Qᵀ   v_mfma_f32_16x16x32_f16; A = K rows straight from HBM (lane: key 16t + li,
+//               dims 32s + 8g .. +8, one 16-B piece), B = fp16(q) (the q the VALU forms
+//               use, unscaled; the exact 1/8 is applied to the fp32 scores)
+//   Oᵀ = Vᵀ·Pᵀ  v_mfma_f32_16x16x16_f16; A = V staged in LDS (swizzled rows), read with
+//               ds_read_b64_tr_b16 (the encoder attention's transposed read); B = P in the
+//               score registers as an fp16 hi/lo pair, two MFMAs, so P keeps ~22 bits as in
+//               the fp32 VALU form
+// Wave w: keys 48w .. 48w+47 (3 tiles of 16) for the scores and for P·V over all 64 dims
+// (one max for the workgroup, exchanged before the exponentials); the 4 waves' P·V sums
+// meet in LDS in fixed order.
+template <int NB>
+__global__ __launch_bounds__(256) void dec_xattn_mfma_kernel(const float* __restrict__ part, int ks,
+                                                             const float* __restrict__ bias,
+                                                             const h16* __restrict__ xk, const h16* __restrict__ xv,
+                                                             int H, int W, int T, int beam, float* __restrict__ ws,
+                                                             int* __restrict__ ticket, h16* __restrict__ out,
+                                                             int64_t lo_off, const SelState* __restrict__ st) {
+    static_assert(NB <= 16 && XKEYS == 192, "16 MFMA columns; 4 waves x 3 key tiles");
+    __shared__ __attribute__((aligned(16))) h16 Vl[XKEYS * HD];
+    __shared__ __attribute__((aligned(16))) h16 qsh[16][HD];
+    __shared__ float red[4][NB][HD];
+    __shared__ float rm[4][16], rl[4][16], bsh[4][HD];
+    __shared__ int last;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, g = lane >> 4, li = lane & 15;
+    const int bid = blockIdx.x;
+    const int chunk = (bid >> 3) & 7;
+    const int p = (bid & 7) + 8 * (bid >> 6);  // (window, head); its 8 chunks share one XCD
+    if (p >= W * H) return;
+    const int h = p % H, w = p / H;
+    {
+        int done = 1;
 #pragma unroll
-        for (int q = 0; q < XCH; ++q) {
-            mm[q] = __hip_atomic_load(src + q * XPART, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            M = fmaxf(M, mm[q]);
-        }
-        float L = 0.f, O = 0.f;
-#pragma unroll
-        for (int q = 0; q < XCH; ++q) {
-            const float e = __expf(mm[q] - M);
-            L = fmaf(__hip_atomic_load(src + q * XPART + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), e, L);
-            O = fmaf(__hip_atomic_load(src + q * XPART + 4 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), e, O);
-        }
-        split_h16(O / L, out, out + lo_off, (int64_t)(r0 + k) * D + h * HD + lane);
+        for (int k = 0; k < NB; ++k)
+            if (k < beam) done &= st[w * beam + k].done;
+        if (done) return;
     }
+    const int D = H * HD;
+    const int per = (T + XCH - 1) / XCH;
+    const int k0 = chunk * per, nk = min(T, k0 + per) - k0;
+    const int64_t hoff = ((int64_t)w * H + h) * T * HD;
+    // q of row r0 + k: fp16(bias + Σ split-K partials), the VALU kernel's order (ks <= 8:
+    // wave wv holds slabs wv and wv + 4).  The slab loads go out first and all at once;
+    // the K/V loads follow, and the barriers before the scores are raw s_barriers: vmcnt
+    // retires loads in issue order, so the q reduction waits for its own loads only,
+    // never for the 48 KB of K/V behind them (a __syncthreads would drain them all).
+    const int r0 = w * beam;
+    const int64_t slab = (int64_t)W * beam * D;
+    float qa[NB], qb[NB];
+    const float bq = bias[h * HD + lane];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+        const int64_t off = (int64_t)(r0 + min(k, beam - 1)) * D + h * HD + lane;
+        qa[k] = part[min(wv, ks - 1) * slab + off];
+        qb[k] = part[min(wv + 4, ks - 1) * slab + off];
+    }
+    // K fragments of this wave's 3 key tiles (A operand), nontemporal, clamped to the chunk
+    h16x8 kf[3][2];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        const int key = k0 + min(16 * (3 * wv + t) + li, nk - 1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+            kf[t][s] = __builtin_nontemporal_load((const h16x8*)(xk + hoff + (int64_t)key * HD + 32 * s + 8 * g));
+    }
+    // V chunk: 24 pieces of 8 rows x 128 B, 6 per wave, into registers now and into LDS
+    // (16-B chunk XOR-swizzled by row) once they land.  Plain loads, not global_load_lds:
+    // with LDS-DMA in flight hipcc drains vmcnt(0) before any use of an earlier load.
+    h16x8 vr[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const int r = (i * 4 + wv) * 8 + (lane >> 3);
+        vr[i] = __builtin_nontemporal_load((const h16x8*)(xv + hoff + (int64_t)(k0 + min(r, nk - 1)) * HD + 8 * (lane & 7)));
+    }
+    const bool has_a = wv < ks, has_b = wv + 4 < ks;
+#pragma unroll
+    for (int k = 0; k < NB; ++k) red[wv][k][lane] = (has_a ? qa[k] : 0.f) + (has_b ? qb[k] : 0.f);
+    bsh[wv][lane] = bq;  // every wave, through LDS: hipcc cannot sink the load past the K/V loads
+    lds_barrier();
+    if (wv == 0) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            h16 q = (h16)0.f;
+            if (k < beam && k < NB) {
+                float r = bsh[0][lane];
+                r += red[0][k][lane] + red[1][k][lane] + red[2][k][lane] + red[3][k][lane];
+                q = (h16)r;
+            }
+            qsh[k][lane] = q;
+        }
+    }
+    lds_barrier();
+    const h16x8 qf0 = *(const h16x8*)&qsh[li][8 * g], qf1 = *(const h16x8*)&qsh[li][32 + 8 * g];
+    // scores: lane holds key 16(3wv + t) + 4g + i of row li
+    f32x4 sc[3];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
+        a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[t][0], qf0, a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[t][1], qf1, a, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int key = 16 * (3 * wv + t) + 4 * g + i;
+            a[i] = key < nk ? a[i] * 0.125f : -INFINITY;
+            mx = fmaxf(mx, a[i]);
+        }
+        sc[t] = a;
+    }
+    mx = fmaxf(mx, xor_lane<16>(mx));
+    mx = fmaxf(mx, xor_lane<32>(mx));
+    if (g == 0) rm[wv][li] = mx;
+    lds_barrier();
+    const float m = fmaxf(fmaxf(rm[0][li], rm[1][li]), fmaxf(rm[2][li], rm[3][li]));
+    // p = exp(s - m) as an fp16 hi/lo pair in the score registers, which are already the
+    // B operand of v_mfma_f32_16x16x16_f16 (lane: keys 4g .. 4g+3 of a tile, row li)
+    float ls = 0.f;
+    h16x4 ph[3], pl[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float pv = __expf(sc[t][i] - m);
+            ls += pv;
+            ph[t][i] = (h16)pv;
+            pl[t][i] = (h16)(pv - (float)ph[t][i]);
+        }
+    ls += xor_lane<16>(ls);
+    ls += xor_lane<32>(ls);
+    if (g == 0) rl[wv][li] = ls;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const int r = (i * 4 + wv) * 8 + (lane >> 3);
+        *(h16x8*)&Vl[r * HD + (((lane & 7) ^ ((r >> 1) & 7)) * 8)] = vr[i];
+    }
+    __syncthreads();
+    // P·V over this wave's 48 keys, all 64 dims: Oᵀ += Vᵀ·Pᵀ, A = V by ds_read_b64_tr_b16
+    // (lane: dim 16dt + li, keys 4g .. 4g+3 of the tile); lane ends with O[li][16dt + 4g + i]
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    {
+        const int q4 = li >> 2, p4 = li & 3;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const int ra = 48 * wv + 16 * t + 4 * g + q4;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                const int col = 16 * dt + 4 * p4;
+                const h16x4 va = ds_read_tr(&Vl[ra * HD + (((col >> 3) ^ ((ra >> 1) & 7)) * 8) + (col & 7)]);
+                o[dt] = __builtin_amdgcn_mfma_f32_16x16x16f16(va, ph[t], o[dt], 0, 0, 0);
+                o[dt] = __builtin_amdgcn_mfma_f32_16x16x16f16(va, pl[t], o[dt], 0, 0, 0);
+            }
+        }
+    }
+    // the 4 waves' key ranges summed in fixed order through LDS (red is free again)
+    if (li < beam && li < NB) {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) *(f32x4*)&red[wv][li][16 * dt + 4 * g] = o[dt];
+    }
+    __syncthreads();
+    if (wv == 0) {
+        // publish (m, l, Σp·v) with device-scope (write-through) stores, wait for them, then
+        // the (window, head) arrival ticket: the 8th arriver merges
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            if (k >= beam) break;
+            float* dst = ws + (((int64_t)(r0 + k) * H + h) * XCH + chunk) * XPART;
+            const float a = (red[0][k][lane] + red[1][k][lane]) + (red[2][k][lane] + red[3][k][lane]);
+            __hip_atomic_store(dst + 4 + lane, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) {
+                const float mk = fmaxf(fmaxf(rm[0][k], rm[1][k]), fmaxf(rm[2][k], rm[3][k]));
+                __hip_atomic_store(dst, mk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(dst + 1, (rl[0][k] + rl[1][k]) + (rl[2][k] + rl[3][k]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        int old = 0;
+        if (lane == 0) old = __hip_atomic_fetch_add(ticket + p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        old = __builtin_amdgcn_readfirstlane(old);
+        if (lane == 0) {
+            last = old == XCH - 1;
+            if (old == XCH - 1) __hip_atomic_store(ticket + p, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    if (!last) return;
+    xattn_merge(ws, r0, beam, H, h, out, lo_off);
 }
 
 // grid B, 256 threads: x[b] += bias + Σ split-K partials (residual stream, fp32), then
@@ -1114,6 +1329,12 @@ void launch_dec_cross_attn(const float* part, int ks, const float* bias, const h
     }
     const int W = B / beam;
     const unsigned grid = (unsigned)(((W * H + 7) / 8) * 8 * XCH);
+    static const bool valu_beam = std::getenv("OSW_XATTN_VALU") != nullptr;  // A/B switch
+    if (beam > 1 && !valu_beam && ks <= 8) {
+        if (beam <= 5) dec_xattn_mfma_kernel<5><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off, st);
+        else dec_xattn_mfma_kernel<8><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off, st);
+        return;
+    }
     switch (beam) {
         case 1: dec_xattn_chunk_kernel<1><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off, st); break;
         case 2: dec_xattn_chunk_kernel<2><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off, st); break;

@@ -42,7 +42,7 @@ constexpr int SEL_SPLIT = 16;  // vocabulary slices per row in the selection ker
 
 void launch_select(const float* logits, int rows, int* pos, const SelParams& P, const int* prompt,
                    const unsigned* supmask, SelState* st, int* cur_tok, int* tokens, int max_tokens, void* sel_parts,
-                   int* arrive, bool bump, hipStream_t s);
+                   int* arrive, bool bump, void* cand, hipStream_t s);
 // the last window's update advances *pos (arrive: a zeroed counter, left zeroed)
 void launch_beam(const float* logits, int windows, int* pos, const SelParams& P, const unsigned* supmask,
                  SelState* st, const void* sel_parts, void* cand, int* seq, int* anc, int ctx, BeamWin* bw,

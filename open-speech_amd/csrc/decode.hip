@@ -989,6 +989,137 @@ __device__ __forceinline__ void select_final_row(const float* __restrict__ logit
     cur_tok[b] = next;
 }
 
+// ---------------------------------------------------------------------------
+// Beam search candidates (restated CTranslate2 BeamSearch, see oracle/decode.py).
+struct BeamCand {
+    float s;
+    int i;  // beam_slice_body: (raw logit, token id); beam_update: (score, beam slot * V + token)
+};
+constexpr int BEAM_SLICES = SEL_SPLIT;  // vocabulary slices per row (one pass: the select slices)
+constexpr int TOPK_VPT = 16;            // logits one thread holds
+constexpr int MAXK2 = 2 * MAX_BEAM;
+static_assert(BEAM_SLICES * 256 * TOPK_VPT >= SEL_SPLIT * 4096, "osw.hip admits V <= SEL_SPLIT * 4096: one batch per slice");
+
+// A beam row's sampling step, one vocabulary slice, ONE pass over its logits: the slice
+// statistics of select_partial_body (same entries in the same order, so the same
+// SelPart) and two candidate lists for beam_update: the slice's top 2*beam tokens by raw
+// logit among the rule-allowed tokens (list A, used when text is allowed) and among the
+// allowed timestamps (list B, used when the timestamp-mass rule suppresses text), each
+// followed by -inf fillers in token order.  Within a row every candidate's score is
+// sum_lp + (x - lse) with one lse per list, monotonic in x, so beam_update ranks these
+// exactly as the former separate top-k pass ranked the scores (score desc, flat index
+// asc); a row whose sum_lp is already -inf (all scores tie at -inf) is the one case
+// where the lists can differ from that pass.
+__device__ __forceinline__ void beam_slice_body(const float* __restrict__ logits, const SelParams& P, int step,
+                                                const unsigned* __restrict__ supmask, const SelState& s,
+                                                SelPart* __restrict__ parts, BeamCand* __restrict__ cand) {
+    __shared__ ArgMax red[2][4];
+    __shared__ SelPart wp[4];
+    const int b = blockIdx.x, sl = blockIdx.y, tid = threadIdx.x;
+    const int K2 = 2 * P.beam;
+    BeamCand* outA = cand + ((int64_t)b * BEAM_SLICES + sl) * 2 * MAXK2;
+    BeamCand* outB = outA + MAXK2;
+    const int per = (P.V + SEL_SPLIT - 1) / SEL_SPLIT;
+    const int lo = sl * per, hi = min(P.V, lo + per);
+    const float* x = logits + (int64_t)b * P.V;
+    float xv[TOPK_VPT];
+    unsigned mw[TOPK_VPT];
+#pragma unroll
+    for (int u = 0; u < TOPK_VPT; ++u) {
+        const int v = min(lo + u * 256 + tid, hi - 1);
+        xv[u] = x[v];
+        mw[u] = supmask[v >> 5];
+    }
+    const RowRules R = row_rules(P, s);
+    float m_all = -INFINITY, s_all = 0.f, m_ts = -INFINITY, s_ts = 0.f;
+    ArgMax a_all{-INFINITY, 0x7fffffff}, a_text{-INFINITY, 0x7fffffff}, a_ts{-INFINITY, 0x7fffffff};
+    unsigned okA = 0, okB = 0, live = 0;  // allowed / allowed timestamp / in slice and not NaN
+#pragma unroll
+    for (int u = 0; u < TOPK_VPT; ++u) {
+        const int v = lo + u * 256 + tid;
+        if (v >= hi) continue;
+        if (xv[u] == xv[u]) live |= 1u << u;
+        if (tok_masked_w(P, R, mw[u], v)) continue;
+        const float xu = xv[u];
+        lse_add(m_all, s_all, xu);
+        a_all = amax(a_all, ArgMax{xu, v});
+        okA |= 1u << u;
+        if (v >= P.tb) {
+            lse_add(m_ts, s_ts, xu);
+            a_ts = amax(a_ts, ArgMax{xu, v});
+            okB |= 1u << u;
+        } else {
+            a_text = amax(a_text, ArgMax{xu, v});
+        }
+    }
+    {  // the slice statistics, merged exactly as select_partial_body merges them
+        auto merge = [&](auto o) {
+            constexpr int O = decltype(o)::value;
+            lse_merge(m_all, s_all, xor_lane<O>(m_all), xor_lane<O>(s_all));
+            lse_merge(m_ts, s_ts, xor_lane<O>(m_ts), xor_lane<O>(s_ts));
+            a_all = amax(a_all, ArgMax{xor_lane<O>(a_all.v), xor_lane<O>(a_all.i)});
+            a_text = amax(a_text, ArgMax{xor_lane<O>(a_text.v), xor_lane<O>(a_text.i)});
+            a_ts = amax(a_ts, ArgMax{xor_lane<O>(a_ts.v), xor_lane<O>(a_ts.i)});
+        };
+        merge(IC<32>{}), merge(IC<16>{}), merge(IC<8>{}), merge(IC<4>{}), merge(IC<2>{}), merge(IC<1>{});
+        if ((tid & 63) == 0)
+            wp[tid >> 6] = SelPart{m_all, s_all, m_ts, s_ts, a_all.v, a_text.v, a_ts.v, a_all.i, a_text.i, a_ts.i};
+    }
+    // top K2 of one list by (key desc, token asc); key = x if allowed, else -inf
+    auto pops = [&](unsigned ok, BeamCand* out) {
+        unsigned used = ~live;
+        auto best = [&]() {
+            int bu = -1;
+            float bv = -INFINITY;
+#pragma unroll
+            for (int u = 0; u < TOPK_VPT; ++u) {
+                const float k = ((ok >> u) & 1u) ? xv[u] : -INFINITY;
+                if (!((used >> u) & 1u) && (bu < 0 || k > bv)) { bv = k; bu = u; }
+            }
+            return bu < 0 ? ArgMax{-INFINITY, INT_MAX} : ArgMax{bv, lo + bu * 256 + tid};
+        };
+        // pop the block-wide best K2 times (wave DPP argmax + one LDS exchange per pop; only
+        // the owner of a popped entry rescans).  (Each wave popping its own top K2 and wave 0
+        // merging the 4*K2 survivors, with no barrier per pop, measured 116 vs 101 us at 320 rows.)
+        ArgMax mine = best();
+        for (int r = 0; r < K2; ++r) {
+            ArgMax a = mine;
+            auto stp = [&](auto o) {
+                constexpr int O = decltype(o)::value;
+                a = amax(a, ArgMax{xor_lane<O>(a.v), xor_lane<O>(a.i)});
+            };
+            stp(IC<32>{}), stp(IC<16>{}), stp(IC<8>{}), stp(IC<4>{}), stp(IC<2>{}), stp(IC<1>{});
+            if ((tid & 63) == 0) red[r & 1][tid >> 6] = a;
+            __syncthreads();
+            ArgMax g = red[r & 1][0];
+#pragma unroll
+            for (int w = 1; w < 4; ++w) g = amax(g, red[r & 1][w]);
+            if (tid == 0) out[r] = BeamCand{g.v, g.i};
+            if (g.i != INT_MAX && mine.i == g.i) {
+                used |= 1u << ((g.i - lo - tid) >> 8);
+                mine = best();
+            }
+        }
+    };
+    pops(okA, outA);
+    if (hi > P.tb) pops(okB, outB);
+    else if (tid < K2) outB[tid] = BeamCand{-INFINITY, INT_MAX};  // no timestamps in this slice
+    __syncthreads();
+    if (tid == 0) {
+        SelPart r = wp[0];
+        for (int i = 1; i < 4; ++i) {
+            const SelPart& q = wp[i];
+            lse_merge(r.m_all, r.s_all, q.m_all, q.s_all);
+            lse_merge(r.m_ts, r.s_ts, q.m_ts, q.s_ts);
+            ArgMax A = amax(ArgMax{r.v_all, r.i_all}, ArgMax{q.v_all, q.i_all});
+            ArgMax X = amax(ArgMax{r.v_text, r.i_text}, ArgMax{q.v_text, q.i_text});
+            ArgMax T = amax(ArgMax{r.v_ts, r.i_ts}, ArgMax{q.v_ts, q.i_ts});
+            r.v_all = A.v; r.i_all = A.i; r.v_text = X.v; r.i_text = X.i; r.v_ts = T.v; r.i_ts = T.i;
+        }
+        parts[b * SEL_SPLIT + sl] = r;  // read by beam_update, a later launch
+    }
+}
+
 // grid (rows, SEL_SPLIT), 256 threads: every slice of a row computes its partial
 // and takes the row's arrival ticket (also slices that have nothing to do, so the
 // finaliser knows every slice has read the step counter); the last one combines the
@@ -1000,8 +1131,19 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ l
                                                      const int* __restrict__ prompt, SelPart* __restrict__ parts,
                                                      SelState* __restrict__ st, int* __restrict__ cur_tok,
                                                      int* __restrict__ tokens, int max_tokens,
-                                                     int* __restrict__ arrive, int* __restrict__ ticket, int bump) {
+                                                     int* __restrict__ arrive, int* __restrict__ ticket, int bump,
+                                                     BeamCand* __restrict__ cand) {
     const int step = *pos_ptr;
+    if (P.beam > 1) {
+        const SelState s = st[blockIdx.x];
+        if (sel_mode(P, step, s) == SEL_SAMPLE) {  // the same for every slice of the row
+            // beam rows' sampling steps: statistics + candidates in one pass; nothing to
+            // finalise here (beam_update picks), so no ticket
+            if (step == P.prompt_len - 1 && blockIdx.x % P.beam != 0) return;  // only the prompt hypothesis expands
+            beam_slice_body(logits, P, step, supmask, s, parts, cand);
+            return;
+        }
+    }
     select_partial_body(logits, P, step, supmask, st, parts);
     __shared__ int last;
     __shared__ SelPart rp[SEL_SPLIT];
@@ -1034,10 +1176,6 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ l
 // finished-hypothesis bookkeeping and the reorder of the surviving hypotheses.
 // The KV cache is never copied: row r's key at position p lives in the slot of row
 // anc[r][p] (written at step p); the reorder copies only anc / tokens / state.
-struct BeamCand {
-    float s;
-    int i;  // flat index within the window: beam slot * V + token
-};
 
 // block-wide argmax (value desc, index asc) of one candidate per thread, 256 threads
 __device__ __forceinline__ ArgMax block_amax(ArgMax a, ArgMax* red) {
@@ -1055,105 +1193,10 @@ __device__ __forceinline__ ArgMax block_amax(ArgMax a, ArgMax* red) {
     return r;
 }
 
-constexpr int BEAM_SLICES = 16;  // vocabulary slices per row in beam_topk
-constexpr int TOPK_VPT = 16;     // logits one thread loads per batch in beam_topk
-constexpr int MAXK2 = 2 * MAX_BEAM;
-static_assert(BEAM_SLICES * 256 * TOPK_VPT >= SEL_SPLIT * 4096, "osw.hip admits V <= SEL_SPLIT * 4096: one batch per slice");
-
-// grid (rows, BEAM_SLICES), 256 threads: the top 2*beam (score desc, flat index asc)
-// of one vocabulary slice of one row.  Each thread loads its TOPK_VPT logits of the
-// slice in one batch (one memory latency instead of one per logit) and scores them
-// in registers; then the block pops its best entry 2*beam times (wave DPP argmax +
-// one LDS exchange per pop; only the owner of a popped entry rescans its slots).
-// A sorted per-thread insertion list cost ~8x more VALU (it ran 141 us here).
-__global__ __launch_bounds__(256) void beam_topk_kernel(const float* __restrict__ logits, SelParams P,
-                                                        const int* __restrict__ pos_ptr,
-                                                        const unsigned* __restrict__ supmask,
-                                                        const SelState* __restrict__ st,
-                                                        const SelPart* __restrict__ parts, BeamCand* __restrict__ cand) {
-    __shared__ float stat[3];
-    __shared__ ArgMax red[2][4];
-    const int row = blockIdx.x, sl = blockIdx.y, tid = threadIdx.x;
-    const int step = *pos_ptr;
-    const SelState s = st[row];
-    if (sel_mode(P, step, s) != SEL_SAMPLE) return;
-    const int K2 = 2 * P.beam, k = row % P.beam;
-    BeamCand* out = cand + ((int64_t)row * BEAM_SLICES + sl) * K2;
-    if (step == P.prompt_len - 1 && k != 0) {  // first sampled step: only the prompt hypothesis expands
-        if (tid < K2) out[tid] = BeamCand{-INFINITY, INT_MAX};
-        return;
-    }
-    if (tid == 0) {
-        const SelPart r = combine_parts<false>(parts + (int64_t)row * SEL_SPLIT);
-        const float lse_all = r.m_all + logf(r.s_all);
-        const float lse_ts = r.m_ts == -INFINITY ? -INFINITY : r.m_ts + logf(r.s_ts);
-        stat[0] = lse_all;
-        stat[1] = lse_ts;
-        stat[2] = (P.with_ts && lse_ts - lse_all > r.v_text - lse_all) ? 1.f : 0.f;
-    }
-    const int per = (P.V + BEAM_SLICES - 1) / BEAM_SLICES;  // <= 256 * TOPK_VPT (host-checked)
-    const int lo = sl * per, hi = min(P.V, lo + per);
-    const float* x = logits + (int64_t)row * P.V;
-    float xv[TOPK_VPT];
-    unsigned mw[TOPK_VPT];  // suppress-mask words, loaded with the logits
-#pragma unroll
-    for (int u = 0; u < TOPK_VPT; ++u) {  // issued before the barrier: overlaps the prelude
-        const int v = lo + u * 256 + tid;
-        xv[u] = v < hi ? x[v] : 0.f;
-        mw[u] = v < hi ? supmask[v >> 5] : 0u;
-    }
-    __syncthreads();
-    const float lse_all = stat[0], lse_ts = stat[1];
-    const bool ts_wins = stat[2] != 0.f;
-    const RowRules R = row_rules(P, s);
-    const int base = k * P.V;
-    // score the thread's logits in place; `used` marks taken, out-of-slice and NaN slots
-    unsigned used = 0;
-#pragma unroll
-    for (int u = 0; u < TOPK_VPT; ++u) {
-        const int v = lo + u * 256 + tid;
-        float lp = -INFINITY;
-        if (!tok_masked_w(P, R, mw[u], v)) {
-            if (!ts_wins) lp = xv[u] - lse_all;
-            else if (v >= P.tb) lp = xv[u] - lse_ts;
-        }
-        xv[u] = s.sum_lp + lp;
-        if (v >= hi || xv[u] != xv[u]) used |= 1u << u;
-    }
-    // the thread's best unused slot (score desc; ascending u = ascending flat index)
-    auto local_best = [&]() {
-        int bu = -1;
-        float bv = -INFINITY;
-#pragma unroll
-        for (int u = 0; u < TOPK_VPT; ++u)
-            if (!((used >> u) & 1u) && (bu < 0 || xv[u] > bv)) { bv = xv[u]; bu = u; }
-        return bu < 0 ? ArgMax{-INFINITY, INT_MAX} : ArgMax{bv, base + lo + bu * 256 + tid};
-    };
-    ArgMax mine = local_best();
-    for (int r = 0; r < K2; ++r) {  // pop the block-wide best K2 times
-        ArgMax a = mine;
-        auto stp = [&](auto o) {
-            constexpr int O = decltype(o)::value;
-            a = amax(a, ArgMax{xor_lane<O>(a.v), xor_lane<O>(a.i)});
-        };
-        stp(IC<32>{}), stp(IC<16>{}), stp(IC<8>{}), stp(IC<4>{}), stp(IC<2>{}), stp(IC<1>{});
-        if ((tid & 63) == 0) red[r & 1][tid >> 6] = a;  // double-buffered: one barrier per pop
-        __syncthreads();
-        ArgMax g = red[r & 1][0];
-#pragma unroll
-        for (int w = 1; w < 4; ++w) g = amax(g, red[r & 1][w]);
-        if (tid == 0) out[r] = BeamCand{g.v, g.i};
-        if (g.i != INT_MAX && mine.i == g.i) {  // flat ids are unique: one owner
-            used |= 1u << ((g.i - base - lo - tid) >> 8);
-            mine = local_best();
-        }
-    }
-}
-
 // grid windows, 256 threads: merge the candidates, register finished hypotheses,
 // pick the surviving beams and reorder their tokens / ancestry / state.
 __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* __restrict__ pos_ptr,
-                                                          SelState* __restrict__ st,
+                                                          SelState* __restrict__ st, const SelPart* __restrict__ parts,
                                                           const BeamCand* __restrict__ cand, int* __restrict__ seq,
                                                           int* __restrict__ anc, int ctx, BeamWin* __restrict__ bwin,
                                                           int* __restrict__ best_tok, int* __restrict__ cur_tok,
@@ -1172,19 +1215,70 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
     const int step = *pos_ptr;
     if (sel_mode(P, step, st[r0]) != SEL_SAMPLE) return;
     const int nc = K * BEAM_SLICES * K2;
-    for (int i = tid; i < nc; i += 256) {
-        const BeamCand c = cand[(int64_t)r0 * BEAM_SLICES * K2 + i];
-        cs[i] = c.s;
-        ci[i] = c.i;
-    }
     const int n = st[r0].n_sampled;  // identical for every row of the window
-    for (int i = tid; i < K * max(n, 1); i += 256) {
-        const int k = i / max(n, 1), j = i % max(n, 1);
-        if (j < n) lseq[k][j] = seq[(int64_t)(r0 + k) * max_tokens + j];
+    // candidates, token histories and ancestry into LDS: 8 loads per thread per round trip
+    // (clamped addresses), stored once they land (a load-then-store loop is one trip each)
+    constexpr int LB = 8;
+    // per row: lse over the allowed tokens, over the allowed timestamps, and the
+    // timestamp-mass rule (the row's 16 slice statistics in fixed order)
+    __shared__ float rlse[MAX_BEAM], rsum[MAX_BEAM];
+    __shared__ int rts[MAX_BEAM];
+    if (tid < K) {
+        rsum[tid] = st[r0 + tid].sum_lp;
+        const SelPart r = combine_parts<false>(parts + (int64_t)(r0 + tid) * SEL_SPLIT);
+        const float lse_all = r.m_all + logf(r.s_all);
+        const float lse_ts = r.m_ts == -INFINITY ? -INFINITY : r.m_ts + logf(r.s_ts);
+        const bool ts_wins = P.with_ts && lse_ts - lse_all > r.v_text - lse_all;
+        rlse[tid] = ts_wins ? lse_ts : lse_all;
+        rts[tid] = ts_wins;
     }
-    for (int i = tid; i < K * step; i += 256) {
-        const int k = i / step, p = i % step;
-        lanc[k][p] = anc[(int64_t)(r0 + k) * ctx + p];
+    __syncthreads();
+    // candidate (row k, slice, j): list B if the row's timestamps win, else list A; score =
+    // sum_lp + (x - lse) as the per-row log-prob + cumulative score of the reference
+    const bool first = step == P.prompt_len - 1;  // only the prompt hypothesis expands
+    for (int i0 = tid; i0 < nc; i0 += 256 * LB) {
+        BeamCand c[LB];
+#pragma unroll
+        for (int j = 0; j < LB; ++j) {
+            const int i = min(i0 + 256 * j, nc - 1), k = i / (BEAM_SLICES * K2), sl = (i / K2) % BEAM_SLICES;
+            c[j] = cand[(((int64_t)(r0 + k) * BEAM_SLICES + sl) * 2 + rts[k]) * MAXK2 + i % K2];
+        }
+#pragma unroll
+        for (int j = 0; j < LB; ++j) {
+            const int i = i0 + 256 * j, k = i / (BEAM_SLICES * K2);
+            if (i >= nc) break;
+            const bool none = c[j].i == INT_MAX || (first && k != 0);
+            cs[i] = none ? -INFINITY : rsum[k] + (c[j].s - rlse[k]);
+            ci[i] = none ? INT_MAX : k * P.V + c[j].i;
+        }
+    }
+    const int nn = max(n, 1), ns = K * nn;
+    for (int i0 = tid; i0 < ns; i0 += 256 * LB) {
+        int v[LB];
+#pragma unroll
+        for (int j = 0; j < LB; ++j) {
+            const int i = min(i0 + 256 * j, ns - 1), k = i / nn, jj = min(i % nn, max_tokens - 1);
+            v[j] = seq[(int64_t)(r0 + k) * max_tokens + jj];
+        }
+#pragma unroll
+        for (int j = 0; j < LB; ++j) {
+            const int i = i0 + 256 * j, k = i / nn, jj = i % nn;
+            if (i < ns && jj < n) lseq[k][jj] = v[j];
+        }
+    }
+    const int na = K * step;
+    for (int i0 = tid; i0 < na; i0 += 256 * LB) {
+        int v[LB];
+#pragma unroll
+        for (int j = 0; j < LB; ++j) {
+            const int i = min(i0 + 256 * j, na - 1);
+            v[j] = anc[(int64_t)(r0 + i / step) * ctx + i % step];
+        }
+#pragma unroll
+        for (int j = 0; j < LB; ++j) {
+            const int i = i0 + 256 * j;
+            if (i < na) lanc[i / step][i % step] = v[j];
+        }
     }
     if (tid < K) lst[tid] = st[r0 + tid];
     __syncthreads();
@@ -1284,13 +1378,13 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
 // the windows; the last one advances the device step counter (every window read it
 // at its start), so beam steps need no separate bump launch.
 __global__ __launch_bounds__(256) void beam_update_kernel(SelParams P, int* __restrict__ pos_ptr,
-                                                          SelState* __restrict__ st,
+                                                          SelState* __restrict__ st, const SelPart* __restrict__ parts,
                                                           const BeamCand* __restrict__ cand, int* __restrict__ seq,
                                                           int* __restrict__ anc, int ctx, BeamWin* __restrict__ bwin,
                                                           int* __restrict__ best_tok, int* __restrict__ cur_tok,
                                                           int max_tokens, int* __restrict__ arrive) {
     const int step = *pos_ptr;
-    beam_update_body(P, pos_ptr, st, cand, seq, anc, ctx, bwin, best_tok, cur_tok, max_tokens);
+    beam_update_body(P, pos_ptr, st, parts, cand, seq, anc, ctx, bwin, best_tok, cur_tok, max_tokens);
     __syncthreads();
     if (threadIdx.x != 0) return;
     __builtin_amdgcn_s_waitcnt(0);
@@ -1310,7 +1404,7 @@ __global__ void count_done_kernel(const SelState* st, int B, int* out) {
 }  // namespace
 
 int sel_parts_bytes() { return (int)sizeof(SelPart) * SEL_SPLIT; }
-int beam_cand_bytes(int beam) { return (int)sizeof(BeamCand) * BEAM_SLICES * 2 * beam; }
+int beam_cand_bytes(int) { return (int)sizeof(BeamCand) * BEAM_SLICES * 2 * MAXK2; }
 
 void launch_dec_self_attn(const float* part, int ks, const float* bias, h16* kc, h16* vc, const int* pos, int B,
                           int H, int ctx, h16* out, int64_t lo_off, const int* anc, int group, const SelState* st,
@@ -1361,19 +1455,19 @@ void launch_dec_reduce_gelu(const float* part, int ks, int B, int N, const float
 
 void launch_select(const float* logits, int rows, int* pos, const SelParams& P, const int* prompt,
                    const unsigned* supmask, SelState* st, int* cur_tok, int* tokens, int max_tokens, void* sel_parts,
-                   int* arrive, bool bump, hipStream_t s) {
-    // arrive[0]: rows finalised this step; arrive[1 + row]: the row's slice tickets
+                   int* arrive, bool bump, void* cand, hipStream_t s) {
+    // arrive[0]: rows finalised this step; arrive[1 + row]: the row's slice tickets; cand:
+    // the beam rows' candidate lists (beam_slice_body)
     select_kernel<<<dim3(rows, SEL_SPLIT), 256, 0, s>>>(logits, P, pos, supmask, prompt, (SelPart*)sel_parts, st,
-                                                        cur_tok, tokens, max_tokens, arrive, arrive + 1, bump ? 1 : 0);
+                                                        cur_tok, tokens, max_tokens, arrive, arrive + 1, bump ? 1 : 0,
+                                                        (BeamCand*)cand);
 }
 
 void launch_beam(const float* logits, int windows, int* pos, const SelParams& P, const unsigned* supmask,
                  SelState* st, const void* sel_parts, void* cand, int* seq, int* anc, int ctx, BeamWin* bw,
                  int* best_tok, int* cur_tok, int max_tokens, int* arrive, hipStream_t s) {
-    beam_topk_kernel<<<dim3(windows * P.beam, BEAM_SLICES), 256, 0, s>>>(logits, P, pos, supmask, st,
-                                                                       (const SelPart*)sel_parts, (BeamCand*)cand);
-    beam_update_kernel<<<windows, 256, 0, s>>>(P, pos, st, (const BeamCand*)cand, seq, anc, ctx, bw, best_tok,
-                                                cur_tok, max_tokens, arrive);
+    beam_update_kernel<<<windows, 256, 0, s>>>(P, pos, st, (const SelPart*)sel_parts, (const BeamCand*)cand, seq,
+                                                anc, ctx, bw, best_tok, cur_tok, max_tokens, arrive);
 }
 
 void launch_count_done(const SelState* st, int rows, int* out, hipStream_t s) {

@@ -163,7 +163,7 @@ struct osw_ctx {
     int* anc = nullptr;        // beam: [R][ctx] row whose cache slot holds position p of this hypothesis
     int* btok = nullptr;       // beam: [B][ctx] best finished hypothesis per window
     BeamWin* bwin = nullptr;   // beam: [B]
-    void* bcand = nullptr;     // beam: [R][SEL_SPLIT][2*beam] candidates
+    void* bcand = nullptr;     // beam: [R][SEL_SPLIT][2 lists][2*MAX_BEAM] candidates (beam_slice_body)
     int* done_host = nullptr;  // pinned
     float* part = nullptr;     // split-K partial slabs of the decoder GEMMs
     float* part2 = nullptr;    // second slab buffer of the fused small-batch step (<= PRO_ROWS rows)
@@ -790,7 +790,7 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
     }
     auto select = [&] {
         launch_select(c->logits, rows, c->pos, SP, c->prompt, c->supmask, c->sel, c->cur_tok, c->tokens, max_tok,
-                      c->selp, c->sel_arrive, beam == 1, c->stream);
+                      c->selp, c->sel_arrive, beam == 1, c->bcand, c->stream);
         if (beam > 1)
             launch_beam(c->logits, nb, c->pos, SP, c->supmask, c->sel, c->selp, c->bcand, c->tokens, c->anc,
                         d.n_text_ctx, c->bwin, c->btok, c->cur_tok, max_tok, c->sel_arrive, c->stream);

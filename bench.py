@@ -66,7 +66,7 @@ def parse():
     ap.add_argument("--realistic-steps", type=int, default=6,
                     help="also time this many steps with realistic output lengths (random weights never emit "
                          "<|endoftext|>: each clip's length is forced from a seeded distribution)")
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_v16_pmc.json"),
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r02_pmc.json"),
                     help="per-kernel HBM bytes from a rocprofv3 --pmc pass (tools/pmc_summary.py)")
     return ap.parse_args()
 

@@ -53,3 +53,85 @@ def test_silence_and_short_clips(backend):
     for pcm in (synth.silence_clip(2.0), synth.tone_clip(0.2), np.zeros(1600, np.int16)):
         r = backend.transcribe(synth.to_wav_bytes(pcm), MID, response_format="verbose_json")
         assert "segments" in r
+
+
+def test_backend_verbose_json_matches_oracle_seek_loop(monkeypatch):
+    """SURVEY §8a rows a1/a5 through the boundary: HipWhisperBackend.transcribe (WAV bytes
+    in, the reference's verbose_json out, src/backends/faster_whisper.py:249-270) on a 75 s
+    clip, greedy, with every window the backend's runner encoded and decoded checked
+    against the oracle's generate_segments restatement (oracle/seek.py) decoding the GPU's
+    own encoder output, and the returned segments equal to the oracle's."""
+    from oracle import decode as odec
+    from oracle import seek as oseek
+    from oracle.model import WhisperOracle
+    from open_speech_amd import dims as D
+    from open_speech_amd import weights
+    from open_speech_amd.engine import WhisperEngine
+    from open_speech_amd.tokenizer import WhisperTokenizer, get_suppressed_tokens
+
+    class Recorder:  # the engine seam the runner drives; records encoder outputs and decode calls
+        def __init__(self, eng):
+            self.eng, self.enc, self.calls, self._wins = eng, {}, [], []
+
+        def __getattr__(self, k):
+            return getattr(self.eng, k)
+
+        def encode(self, wins):
+            self._wins = list(wins)
+            self.eng.encode(wins)
+            for k, (_c, seek, size) in enumerate(wins):
+                self.enc[(seek, size)] = self.eng.encoder_output(k)
+
+        def decode(self, n, cfg, prefix=None, dump_steps=0, languages=None):
+            outs = self.eng.decode(n, cfg, prefix=prefix, languages=languages)
+            for k, w in enumerate(self._wins):
+                self.calls.append((w[1], w[2], list(prefix[k]) if prefix else [], outs[k]))
+            return outs
+
+    recs = []
+
+    def factory(dims, gpu, max_batch):
+        r = Recorder(WhisperEngine(dims, device=gpu, max_batch=max_batch))
+        recs.append(r)
+        return r
+
+    monkeypatch.setenv("STT_HIP_BEAM_SIZE", "1")
+    monkeypatch.setenv("STT_HIP_MAX_BATCH", "2")
+    monkeypatch.setenv("STT_HIP_GPUS", "0")
+    monkeypatch.setenv("STT_HIP_LANES", "1")  # one lane: every window goes through the recorder
+    b = HipWhisperBackend(engine_factory=factory)
+    b.load_model(MID)
+    try:
+        pcm = synth.chirp_clip(41, 75.0)
+        r = b.transcribe(synth.to_wav_bytes(pcm), MID, response_format="verbose_json")
+    finally:
+        b.unload_model(MID)
+    assert len(recs) == 1
+    rec = recs[0]
+    assert len(rec.calls) >= 3, "a 75 s clip needs at least three 30 s windows"
+    d = D.TINY_TEST
+    w = weights.random_weights(d, seed=1234)  # the values init_random(seed=1234) writes on the device
+    tok = WhisperTokenizer(d.n_vocab)
+    st = tok.special
+    sup = get_suppressed_tokens(tok, [-1])
+    orc = WhisperOracle(d, w, fp16=True)
+    gpu = {(s, z): (p, o) for s, z, p, o in rec.calls}
+    lang = {}
+
+    def decode_window(seek, size, prompt):
+        enc = rec.enc[(seek, size)]
+        o = odec.greedy_from_encoder(orc, orc.cross_kv(enc), st, language=lang.get("tok"),
+                                     prev_tokens=prompt[1:], opts=odec.DecodeOptions(suppress_tokens=sup))
+        lang.setdefault("tok", o.language)
+        gp, go = gpu[(seek, size)]
+        assert gp == prompt, f"window {seek}: prompt differs"
+        assert go.tokens == o.tokens, f"window {seek}: ids differ from the oracle's"
+        return go.tokens, go.sum_logprob, go.no_speech_prob
+
+    nf = (len(pcm) + 160) // 160
+    wins = oseek.seek_loop(decode_window, nf, st, tok.decode)
+    want = [(a, b_, t) for x in wins for a, b_, t in x.segments]
+    got = [(s["start"], s["end"], s["tokens"]) for s in r["segments"]]
+    assert [(round(a, 6), round(e, 6), t) for a, e, t in got] == [(round(a, 6), round(e, 6), t) for a, e, t in want]
+    assert r["task"] == "transcribe" and r["duration"] == pytest.approx(75.0)
+    assert [s["id"] for s in r["segments"]] == list(range(len(r["segments"])))

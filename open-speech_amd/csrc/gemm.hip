@@ -857,20 +857,42 @@ __global__ __launch_bounds__(256, 2) void gemm_wide_kernel(GemmArgs g) {
     }
     float* C = (float*)g.C + (g.kc > 0 ? (int64_t)blockIdx.z * g.M * g.ldc : 0);
     const float* bias = g.kc > 0 ? nullptr : g.bias;
+    // the 64 x 128 fp32 tile leaves through LDS (the W ring, free once every wave is past
+    // its last K tile) as 8-B device-scope (write-through) stores, 512 B contiguous per
+    // wave-instruction: the MFMA layout's 4-B stores scattered over 4 rows took ~half of
+    // the beam logits GEMM (66 MB of fp32 at 320 rows).  Rows stay 8-B aligned for the
+    // vocabulary's row stride (51866 floats), not 16-B.
+    constexpr int TS = 2 * WBM + 2;  // LDS row stride (floats) of the 64 x 128 tile
+    static_assert(WBM * TS * 4 <= WSL * WBN * BK * 2, "the tile fits the W ring");
+    float* T = (float*)&lw[0][0];
+    __syncthreads();
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int m = m0 + mi * 16 + (lane >> 4) * 4 + i;
-            if (m >= g.M) continue;
+            const int row = mi * 16 + (lane >> 4) * 4 + i;
 #pragma unroll
             for (int ni = 0; ni < 2; ++ni) {
-                const int n = n0 + wave * 32 + ni * 16 + (lane & 15);
-                if (n >= g.N) continue;
-                const float v = bias ? acc[mi][ni][i] + bias[n] : acc[mi][ni][i];
-                __hip_atomic_store(C + (int64_t)m * g.ldc + n, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int col = wave * 32 + ni * 16 + (lane & 15);
+                const int n = min(n0 + col, g.N - 1);
+                T[row * TS + col] = bias ? acc[mi][ni][i] + bias[n] : acc[mi][ni][i];
             }
         }
+    __syncthreads();
+#pragma unroll 4
+    for (int f = threadIdx.x; f < WBM * WBN / 2; f += 256) {
+        const int row = f / (WBN / 2), c2 = (f % (WBN / 2)) * 2;
+        const int m = m0 + row, n = n0 + c2;
+        if (m >= g.M || n >= g.N) continue;
+        float* dst = C + (int64_t)m * g.ldc + n;
+        if (n + 1 < g.N) {
+            const unsigned long long bits = (unsigned long long)__float_as_uint(T[row * TS + c2]) |
+                                            ((unsigned long long)__float_as_uint(T[row * TS + c2 + 1]) << 32);
+            __hip_atomic_store((unsigned long long*)dst, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(dst, T[row * TS + c2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 void launch_wide(const GemmArgs& g, int ks, hipStream_t s) {

@@ -90,7 +90,11 @@ __global__ __launch_bounds__(256, 2) void enc_attn_kernel(const h16* __restrict_
     stage(0, 0);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-    for (int kt = 0; kt < nkt; ++kt) {
+    // one K/V tile; TAIL: the last one, whose keys past T are masked (a separate
+    // instantiation: the masking selects cost ~50 VALU ops per tile in every tile when the
+    // condition was a runtime flag, in a VALU-bound loop)
+    auto tile = [&](int kt, auto tail_c) {
+        constexpr bool tail = decltype(tail_c)::value;
         const int buf = kt & 1;
         if (kt + 1 < nkt) stage(buf ^ 1, (kt + 1) * KB);
         const h16* Kl = lds[buf][0];
@@ -117,7 +121,6 @@ __global__ __launch_bounds__(256, 2) void enc_attn_kernel(const h16* __restrict_
         // kept on raw scores and the 1/sqrt(d)*log2(e) scale folds into one FMA per score,
         // keys past T are masked only in the last tile, and exp2 is the bare v_exp_f32
         // (results below 2^-126 flush to 0, irrelevant next to the row maximum's 1).
-        const bool tail = k0 + KB > T;
         h16x8 pf[2][2];
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) {
@@ -126,7 +129,8 @@ __global__ __launch_bounds__(256, 2) void enc_attn_kernel(const h16* __restrict_
             for (int t = 0; t < 4; ++t)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    if (tail && k0 + 16 * t + 4 * g + i >= T) sc[qt][t][i] = -INFINITY;
+                    if constexpr (tail)
+                        if (k0 + 16 * t + 4 * g + i >= T) sc[qt][t][i] = -INFINITY;
                     mx = fmaxf(mx, sc[qt][t][i]);
                 }
             mx = fmaxf(mx, xor_lane<16>(mx));
@@ -183,7 +187,10 @@ __global__ __launch_bounds__(256, 2) void enc_attn_kernel(const h16* __restrict_
         }
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
-    }
+    };
+    const bool last_partial = nkt * KB > T;
+    for (int kt = 0; kt < nkt - (last_partial ? 1 : 0); ++kt) tile(kt, std::false_type{});
+    if (last_partial) tile(nkt - 1, std::true_type{});
 
     // ---- normalise and store: lane holds O[q = li][d = 16 dt + 4 g + i]
     const int D = H * HD;

@@ -57,18 +57,24 @@ __device__ __forceinline__ void store_one(const GemmArgs& g, int m, int n, float
     }
 }
 
-template <int EPI>
+// TM = 128 (the default) or 64: the 64x64 tile for small M (the encoder of one or a few
+// windows: 1500 rows give a 128-tile N = 1280 GEMM only 120 workgroups for 256 CUs).
+// Every output element is the same MFMA chain over K in the same order at either tile
+// size (and in the 256-tile kernels), so the choice never changes a result.
+template <int EPI, int TM = BM>
 __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
-    __shared__ __attribute__((aligned(16))) h16 lds[2][2][BM * BK];  // [buf][A|W], 64 KiB
+    constexpr int PW = TM / 32;  // glds pieces (8 rows x 128 B) per wave per operand
+    constexpr int FT = TM / 32;  // 16x16 fragments per wave per dimension (2x2 waves)
+    __shared__ __attribute__((aligned(16))) h16 lds[2][2][TM * BK];  // [buf][A|W]
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+    const int n0 = blockIdx.x * TM, m0 = blockIdx.y * TM;
     const int kc = g.kc > 0 ? g.kc : g.K, kbeg = blockIdx.z * kc;  // split-K: slab blockIdx.z
 
-    // per-thread source rows for the 4 A and 4 W glds pieces (fixed over K)
-    const h16* asrc[4];
-    const h16* wsrc[4];
+    // per-thread source rows for the A and W glds pieces (fixed over K)
+    const h16* asrc[PW];
+    const h16* wsrc[PW];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < PW; ++i) {
         const int r = (i * 4 + wave) * 8 + (lane >> 3);
         const int c = swz(r, lane & 7);
         const int gm = min(m0 + r, g.M - 1);
@@ -79,7 +85,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
 
     auto stage = [&](int buf, int k0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < PW; ++i) {
             h16* da = &lds[buf][0][(i * 4 + wave) * 8 * BK];
             h16* dw = &lds[buf][1][(i * 4 + wave) * 8 * BK];
             __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + k0), (OSW_LDS void*)da, 16, 0, 0);
@@ -88,11 +94,12 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
     };
 
     const int wm = wave >> 1, wn = wave & 1;
-    f32x4 acc[4][4];
+    constexpr int WT = TM / 2;  // wave tile edge
+    f32x4 acc[FT][FT];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < FT; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < FT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const int nk = kc / BK;
     stage(0, 0);
@@ -106,21 +113,21 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             const int c = ks * 4 + (lane >> 4);
-            h16x8 a[4], b[4];
+            h16x8 a[FT], b[FT];
 #pragma unroll
-            for (int mi = 0; mi < 4; ++mi) {
-                const int row = wm * 64 + mi * 16 + (lane & 15);
+            for (int mi = 0; mi < FT; ++mi) {
+                const int row = wm * WT + mi * 16 + (lane & 15);
                 a[mi] = *(const h16x8*)&la[row * BK + swz(row, c) * 8];
             }
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni) {
-                const int row = wn * 64 + ni * 16 + (lane & 15);
+            for (int ni = 0; ni < FT; ++ni) {
+                const int row = wn * WT + ni * 16 + (lane & 15);
                 b[ni] = *(const h16x8*)&lw[row * BK + swz(row, c) * 8];
             }
 #pragma unroll
-            for (int mi = 0; mi < 4; ++mi)
+            for (int mi = 0; mi < FT; ++mi)
 #pragma unroll
-                for (int ni = 0; ni < 4; ++ni)
+                for (int ni = 0; ni < FT; ++ni)
                     acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
         }
         __builtin_amdgcn_s_waitcnt(0);
@@ -130,14 +137,14 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
     if (EPI == EPI_F32 && g.kc > 0) {  // split-K partial slab: plain stores, no bias
         float* C = (float*)g.C + (int64_t)blockIdx.z * g.M * g.ldc;
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
+        for (int mi = 0; mi < FT; ++mi)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int m = m0 + wm * 64 + mi * 16 + (lane >> 4) * 4 + i;
+                const int m = m0 + wm * WT + mi * 16 + (lane >> 4) * 4 + i;
                 if (m >= g.M) continue;
 #pragma unroll
-                for (int ni = 0; ni < 4; ++ni) {
-                    const int n = n0 + wn * 64 + ni * 16 + (lane & 15);
+                for (int ni = 0; ni < FT; ++ni) {
+                    const int n = n0 + wn * WT + ni * 16 + (lane & 15);
                     if (n < g.N)  // written through L2, like the skinny slabs
                         __hip_atomic_store(&C[(int64_t)m * g.ldc + n], acc[mi][ni][i], __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
@@ -146,14 +153,14 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
         return;
     }
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < FT; ++mi)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int m = m0 + wm * 64 + mi * 16 + (lane >> 4) * 4 + i;
+            const int m = m0 + wm * WT + mi * 16 + (lane >> 4) * 4 + i;
             if (m >= g.M) continue;
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni) {
-                const int n = n0 + wn * 64 + ni * 16 + (lane & 15);
+            for (int ni = 0; ni < FT; ++ni) {
+                const int n = n0 + wn * WT + ni * 16 + (lane & 15);
                 if (n >= g.N) continue;
                 if constexpr (EPI == EPI_F32) {  // decoder logits: written through L2 for the select kernels
                     const float v = g.bias ? acc[mi][ni][i] + g.bias[n] : acc[mi][ni][i];
@@ -1068,6 +1075,22 @@ void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s) {
             case EPI_F32: launch256<EPI_F32>(g, s); return;
             default: launch256<EPI_HEADS>(g, s); return;
         }
+    }
+    // fewer than 2 workgroups per CU on the 128 tile (small M: one or a few encoder
+    // windows): the 64 tile, 4x the workgroups, identical results
+    static const bool no_small = getenv("OSW_NO_TILE64") != nullptr;  // A/B switch
+    const int64_t tiles128 = (int64_t)((g.N + BN - 1) / BN) * ((g.M + BM - 1) / BM);
+    if (variant == 6 || (!no_small && variant == 0 && g.kc == 0 && tiles128 < 512)) {
+        dim3 grid((g.N + 63) / 64, (g.M + 63) / 64);
+        switch (g.epi) {
+            case EPI_F16: gemm_kernel<EPI_F16, 64><<<grid, NTHR, 0, s>>>(g); break;
+            case EPI_F16_GELU: gemm_kernel<EPI_F16_GELU, 64><<<grid, NTHR, 0, s>>>(g); break;
+            case EPI_F32_RESID: gemm_kernel<EPI_F32_RESID, 64><<<grid, NTHR, 0, s>>>(g); break;
+            case EPI_F32_GELU_POS: gemm_kernel<EPI_F32_GELU_POS, 64><<<grid, NTHR, 0, s>>>(g); break;
+            case EPI_F32: gemm_kernel<EPI_F32, 64><<<grid, NTHR, 0, s>>>(g); break;
+            default: gemm_kernel<EPI_HEADS, 64><<<grid, NTHR, 0, s>>>(g); break;
+        }
+        return;
     }
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
     switch (g.epi) {

@@ -18,6 +18,7 @@
 #include "resln.h"
 
 #include <cstdlib>
+#include <stdexcept>
 
 namespace osw {
 
@@ -575,6 +576,102 @@ __device__ __forceinline__ void wait_vmcnt() {
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
+// Small-M encoder GEMM (one or a few windows): 64x64 tiles (4 waves of 32x32) with a
+// 4-slot LDS ring that keeps three K tiles in flight.  A 64-tile K step is only 8 MFMAs
+// per wave, far shorter than the load latency, so the double-buffered gemm_kernel<.., 64>
+// waited ~one HBM round trip per K step (fc2 at 1500 rows: 80 steps, ~70 us).  Counted
+// vmcnt + raw s_barrier (a __syncthreads would drain every LDS-DMA in flight).  The
+// MFMA chain of every output element is gemm_kernel's, in the same K order: identical
+// results.
+constexpr int R64_NS = 4;
+template <int EPI>
+__global__ __launch_bounds__(NTHR, 2) void gemm64_ring_kernel(GemmArgs g) {
+    constexpr int TM = 64, PW = 2, FT = 2, WT = 32;
+    __shared__ __attribute__((aligned(16))) h16 lds[R64_NS][2][TM * BK];  // 64 KiB
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int n0 = blockIdx.x * TM, m0 = blockIdx.y * TM;
+    const h16* asrc[PW];
+    const h16* wsrc[PW];
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+        const int r = (i * 4 + wave) * 8 + (lane >> 3);
+        const int c = swz(r, lane & 7);
+        asrc[i] = grp_row(g.A, min(m0 + r, g.M - 1), g.a_grp_rows, g.a_grp_stride, g.lda) + c * 8;
+        wsrc[i] = g.W + (int64_t)min(n0 + r, g.N - 1) * g.ldw + c * 8;
+    }
+    auto stage = [&](int slot, int k0) {
+#pragma unroll
+        for (int i = 0; i < PW; ++i) {
+            __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + k0), (OSW_LDS void*)&lds[slot][0][(i * 4 + wave) * 8 * BK],
+                                             16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + k0), (OSW_LDS void*)&lds[slot][1][(i * 4 + wave) * 8 * BK],
+                                             16, 0, 0);
+        }
+    };
+    const int wm = wave >> 1, wn = wave & 1;
+    f32x4 acc[FT][FT];
+#pragma unroll
+    for (int i = 0; i < FT; ++i)
+#pragma unroll
+        for (int j = 0; j < FT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nk = g.K / BK;
+#pragma unroll
+    for (int s = 0; s < R64_NS - 1; ++s)
+        if (s < nk) stage(s, s * BK);
+    for (int kt = 0; kt < nk; ++kt) {
+        // tile kt has landed once at most min(NS-2, nk-1-kt) younger tiles are in flight
+        const int ahead = min(R64_NS - 2, nk - 1 - kt);
+        if (ahead >= 2) wait_vmcnt<2 * 2 * PW>();
+        else if (ahead == 1) wait_vmcnt<2 * PW>();
+        else wait_vmcnt<0>();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave's pieces of tile kt landed; slot (kt-1) % NS is free
+        asm volatile("" ::: "memory");
+        if (kt + R64_NS - 1 < nk) stage((kt + R64_NS - 1) % R64_NS, (kt + R64_NS - 1) * BK);
+        const h16* la = lds[kt % R64_NS][0];
+        const h16* lw = lds[kt % R64_NS][1];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int c = ks * 4 + (lane >> 4);
+            h16x8 a[FT], b[FT];
+#pragma unroll
+            for (int mi = 0; mi < FT; ++mi) {
+                const int row = wm * WT + mi * 16 + (lane & 15);
+                a[mi] = *(const h16x8*)&la[row * BK + swz(row, c) * 8];
+            }
+#pragma unroll
+            for (int ni = 0; ni < FT; ++ni) {
+                const int row = wn * WT + ni * 16 + (lane & 15);
+                b[ni] = *(const h16x8*)&lw[row * BK + swz(row, c) * 8];
+            }
+#pragma unroll
+            for (int mi = 0; mi < FT; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < FT; ++ni)
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int mi = 0; mi < FT; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int m = m0 + wm * WT + mi * 16 + (lane >> 4) * 4 + i;
+            if (m >= g.M) continue;
+#pragma unroll
+            for (int ni = 0; ni < FT; ++ni) {
+                const int n = n0 + wn * WT + ni * 16 + (lane & 15);
+                if (n >= g.N) continue;
+                if constexpr (EPI == EPI_F32) {
+                    const float v = g.bias ? acc[mi][ni][i] + g.bias[n] : acc[mi][ni][i];
+                    const int64_t grp = m / g.c_grp_rows, r = m % g.c_grp_rows;
+                    __hip_atomic_store((float*)g.C + grp * g.c_grp_stride + r * g.ldc + n, v, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                } else
+                    store_one<EPI>(g, m, n, acc[mi][ni][i]);
+            }
+        }
+}
+
 template <int MT, bool DIRECT, int EPI, bool LO, int PRO = PRO_NONE>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, float* __restrict__ part, ProArgs pa) {
     // Workgroup = 64 columns x one kc-deep K range; wave = 16 columns.  The
@@ -602,7 +699,9 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
     constexpr int NIMG = LO ? 2 : 1;
     constexpr int APIECES = ROWS / RPP / 4;      // glds per wave per image per chunk
     __shared__ __attribute__((aligned(16))) h16 As[PRO ? 1 : 2][NIMG][PRO ? 8 : ROWS * CKK];
-    __shared__ __attribute__((aligned(16))) h16 Ap[PRO ? 2 : 1][PRO ? PRO_ROWS : 1][PRO ? PRO_STRIDE : 8];
+    constexpr int APR = PRO == PRO_GELU ? GELU_ROWS : PRO == PRO_RESLN ? PRO_ROWS : 1;  // image rows
+    constexpr int APS = PRO == PRO_GELU ? GELU_KC + 8 : PRO == PRO_RESLN ? PRO_STRIDE : 8;
+    __shared__ __attribute__((aligned(16))) h16 Ap[PRO ? 2 : 1][APR][APS];
     __shared__ float pred[PRO ? 2 * PRO_ROWS * 4 : 1];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nb = blockIdx.x * 64 + wave * 16;
@@ -698,16 +797,23 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
         __syncthreads();
     } else if constexpr (PRO == PRO_GELU) {
         const int64_t slab = (int64_t)g.M * g.K;
-#pragma unroll
-        for (int r = 0; r < PRO_ROWS; ++r) {
-            if (r >= g.M) break;
+        auto rows = [&](auto nr) {
+            constexpr int NR = decltype(nr)::value;
             for (int j = threadIdx.x; j < kc; j += 256) {
-                const float y = gelu_reduce_one(pa.part, pa.ks, slab, pa.bias, (int64_t)r * g.K + k0 + j, k0 + j);
-                const h16 h = (h16)y;
-                Ap[0][r][j] = h;
-                Ap[PRO ? 1 : 0][r][j] = (h16)(y - (float)h);
+                float y[NR];
+                gelu_reduce_rows<NR>(pa.part, pa.ks, slab, pa.bias, g.M, g.K, k0 + j, y);
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const h16 h = (h16)y[r];
+                    Ap[0][r][j] = h;
+                    Ap[PRO ? 1 : 0][r][j] = (h16)(y[r] - (float)h);
+                }
             }
-        }
+        };
+        if (g.M <= 1) rows(std::integral_constant<int, 1>{});
+        else if (g.M <= 2) rows(std::integral_constant<int, 2>{});
+        else if (g.M <= 4) rows(std::integral_constant<int, 4>{});
+        else rows(std::integral_constant<int, GELU_ROWS>{});
         __syncthreads();
     }
     for (int c = 0; c < nch; c += 2) {
@@ -986,13 +1092,15 @@ int launch_gemm_skinny_partial(const GemmArgs& g, float* part, hipStream_t s) {
 // by the consumer kernel exactly like the skinny kernel's slabs.  Picks the largest
 // split (K/ks a multiple of 64, >= 256 deep) that keeps the grid near 1024 workgroups
 // (2 per CU).
-// Fused small-batch form (<= PRO_ROWS hi/lo rows): the operand is built by the prologue
-// (resln.h).  direct: one K range, EPI_F32 straight into g.C (the logits); otherwise the
+// Fused small-batch form (<= PRO_ROWS hi/lo rows for PRO_RESLN, <= GELU_ROWS for PRO_GELU):
+// the operand is built by the prologue (resln.h).  direct: one K range, EPI_F32 straight into g.C (the logits); otherwise the
 // split-K slabs into part, as launch_gemm_skinny_partial.  Returns ksplit.
 int launch_gemm_skinny_pro(const GemmArgs& g, int pro, const ProArgs& pa, bool direct, float* part, hipStream_t s) {
     const int ks = direct ? 1 : skinny_ksplit(g.N, g.K);
     const dim3 grid((g.N + 63) / 64, ks, 1);
     const int kc = g.K / ks;
+    if (pro == PRO_GELU ? g.M > GELU_ROWS || kc > GELU_KC : g.M > PRO_ROWS)
+        throw std::invalid_argument("fused GEMM prologue: rows or K range exceed its LDS image");
     if (direct) {
         if (pro == PRO_RESLN) gemm_skinny_kernel<1, true, EPI_F32, true, PRO_RESLN><<<grid, 256, 0, s>>>(g, kc, part, pa);
         else gemm_skinny_kernel<1, true, EPI_F32, true, PRO_GELU><<<grid, 256, 0, s>>>(g, kc, part, pa);
@@ -1080,8 +1188,22 @@ void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s) {
     // windows): the 64 tile, 4x the workgroups, identical results
     static const bool no_small = getenv("OSW_NO_TILE64") != nullptr;  // A/B switch
     const int64_t tiles128 = (int64_t)((g.N + BN - 1) / BN) * ((g.M + BM - 1) / BM);
-    if (variant == 6 || (!no_small && variant == 0 && g.kc == 0 && tiles128 < 512)) {
+    if (variant == 6 || variant == 7 || (!no_small && variant == 0 && g.kc == 0 && tiles128 < 512)) {
         dim3 grid((g.N + 63) / 64, (g.M + 63) / 64);
+        // the 4-slot ring (64 KB, 2 workgroups per CU) for long K (fc2: 70 -> 45 us at one
+        // window); at K = 1280 the double-buffered kernel's occupancy wins (qkv 43 vs 50 us)
+        static const bool no_ring = getenv("OSW_NO_RING64") != nullptr;  // A/B switch
+        if (variant == 6 || (variant == 0 && !no_ring && g.K > 2048)) {
+            switch (g.epi) {
+                case EPI_F16: gemm64_ring_kernel<EPI_F16><<<grid, NTHR, 0, s>>>(g); break;
+                case EPI_F16_GELU: gemm64_ring_kernel<EPI_F16_GELU><<<grid, NTHR, 0, s>>>(g); break;
+                case EPI_F32_RESID: gemm64_ring_kernel<EPI_F32_RESID><<<grid, NTHR, 0, s>>>(g); break;
+                case EPI_F32_GELU_POS: gemm64_ring_kernel<EPI_F32_GELU_POS><<<grid, NTHR, 0, s>>>(g); break;
+                case EPI_F32: gemm64_ring_kernel<EPI_F32><<<grid, NTHR, 0, s>>>(g); break;
+                default: gemm64_ring_kernel<EPI_HEADS><<<grid, NTHR, 0, s>>>(g); break;
+            }
+            return;
+        }
         switch (g.epi) {
             case EPI_F16: gemm_kernel<EPI_F16, 64><<<grid, NTHR, 0, s>>>(g); break;
             case EPI_F16_GELU: gemm_kernel<EPI_F16_GELU, 64><<<grid, NTHR, 0, s>>>(g); break;

@@ -461,7 +461,7 @@ void setup_workspace(osw_ctx* c) {
         int64_t p2 = 0;
         for (auto& nk : shapes)
             if (nk[0] != d.n_vocab) p2 = std::max<int64_t>(p2, (int64_t)skinny_ksplit((int)nk[0], (int)nk[1]) * nk[0]);
-        c->part2 = dalloc<float>(p2 * std::min<int64_t>(R, PRO_ROWS), o);
+        c->part2 = dalloc<float>(p2 * std::min<int64_t>(R, GELU_ROWS), o);
     }
     HIPCHK(hipHostMalloc((void**)&c->done_host, sizeof(int), 0));
 }
@@ -679,6 +679,8 @@ void decoder_step(osw_ctx* c, int nb, int group, bool gather) {
         decoder_step_fused(c, nb, group, gather);
         return;
     }
+    static const bool no_gelu_pro = getenv("OSW_NO_GELU_PRO") != nullptr;  // A/B switch
+    const bool gelu_pro = nb <= GELU_ROWS && !no_gelu_pro && 4 * D / skinny_ksplit(D, 4 * D) <= GELU_KC;
     // x = tok_emb[tok] + pos_emb[pos]; xdn = LN1_0(x)
     launch_dec_resid_ln(nullptr, 0, nb, D, nullptr, c->xd, WF(c, "dec.l0.ln1.g"), WF(c, "dec.l0.ln1.b"), c->xdn, lo_d,
                         WH(c, "dec.tok"), WF(c, "dec.pos"), c->cur_tok, c->pos, ctx, c->stream);
@@ -703,10 +705,21 @@ void decoder_step(osw_ctx* c, int nb, int group, bool gather) {
         // (a whole-K fc1 with the GELU epilogue fused has only N/64 = 80 workgroups at
         // turbo: 22.7 us vs 9.6 + 4.7 us for split-K + reduce, measured)
         ks = partial(c->xdn, D, WH(c, p + ".fc1.w"), 4 * D, D);
-        launch_dec_reduce_gelu(c->part, ks, nb, 4 * D, WF(c, p + ".fc1.b"), c->dh, lo_4d, c->stream);
-        ks = partial(c->dh, 4 * D, WH(c, p + ".fc2.w"), D, 4 * D);
+        const float* fc2_part = c->part;
+        if (gelu_pro) {
+            // <= 8 rows: the GELU reduce is fc2's prologue (each workgroup reduces only its own
+            // K range of the fc1 slabs, resln.h), fc2's slabs go to part2
+            ProArgs pg{};
+            pg.part = c->part; pg.ks = ks; pg.bias = WF(c, p + ".fc1.b");
+            GemmArgs g = gemm_plain(nullptr, D, WH(c, p + ".fc2.w"), nullptr, nb, D, 4 * D, nullptr, 0, EPI_F32);
+            ks = launch_gemm_skinny_pro(g, PRO_GELU, pg, false, c->part2, c->stream);
+            fc2_part = c->part2;
+        } else {
+            launch_dec_reduce_gelu(c->part, ks, nb, 4 * D, WF(c, p + ".fc1.b"), c->dh, lo_4d, c->stream);
+            ks = partial(c->dh, 4 * D, WH(c, p + ".fc2.w"), D, 4 * D);
+        }
         const std::string nx = l + 1 < L ? "dec.l" + std::to_string(l + 1) + ".ln1" : std::string("dec.lnpost");
-        launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".fc2.b"), c->xd, WF(c, nx + ".g"), WF(c, nx + ".b"), c->xdn,
+        launch_dec_resid_ln(fc2_part, ks, nb, D, WF(c, p + ".fc2.b"), c->xd, WF(c, nx + ".g"), WF(c, nx + ".b"), c->xdn,
                             lo_d, nullptr, nullptr, nullptr, nullptr, ctx, c->stream);
     }
     GemmArgs gl = gemm_plain(c->xdn, D, WH(c, "dec.tok"), nullptr, nb, d.n_vocab, D, c->logits, d.n_vocab, EPI_F32);

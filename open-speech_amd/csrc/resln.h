@@ -149,6 +149,8 @@ enum Pro : int { PRO_NONE = 0, PRO_RESLN = 1, PRO_GELU = 2 };
 constexpr int PRO_ROWS = 1;      // rows the prologue serves: batch-1 latency (every workgroup
                                  // re-reads all rows' slabs, so 5 beam rows were slower, measured)
 constexpr int PRO_STRIDE = 1288; // halfs per LDS image row (D <= 1280; +8 staggers the banks)
+constexpr int GELU_ROWS = 8;     // PRO_GELU serves up to 8 rows: each workgroup reduces only its
+constexpr int GELU_KC = 256;     // own K range (<= GELU_KC deep), so no slab is read twice
 struct ProArgs {
     ResLnArgs ln;        // PRO_RESLN: LayerNorm(x') of every row, all D columns
     const float* part;   // PRO_GELU: the fc1 slabs [ks][M][K], K = this GEMM's K
@@ -169,6 +171,29 @@ __device__ __forceinline__ float gelu_reduce_one(const float* part, int ks, int6
         for (int j = 0; j < 8; ++j) v += k0 + j < ks ? p[j] : 0.f;
     }
     return gelu_erf(v);
+}
+
+// gelu_reduce_one for NR rows at once (rows past M repeat row M-1): every row's slab loads
+// of a batch of 8 slabs are in flight together, the adds per row in gelu_reduce_one's order
+template <int NR>
+__device__ __forceinline__ void gelu_reduce_rows(const float* part, int ks, int64_t slab, const float* bias, int M,
+                                                 int64_t ld, int64_t col, float (&y)[NR]) {
+    const float b = bias[col];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) y[r] = b;
+    for (int k0 = 0; k0 < ks; k0 += 8) {
+        float p[NR][8];
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) p[r][j] = part[(int64_t)min(k0 + j, ks - 1) * slab + min(r, M - 1) * ld + col];
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) y[r] += k0 + j < ks ? p[r][j] : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r) y[r] = gelu_erf(y[r]);
 }
 
 }  // namespace osw

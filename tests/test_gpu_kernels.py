@@ -24,7 +24,8 @@ def eng():
     (3, 1, 1280, 1280), (3, 7, 51866, 384), (3, 64, 5120, 1280), (3, 33, 1280, 5120), (0, 5, 300, 256),
     (3, 64, 51866, 1280), (3, 16, 384, 1536), (3, 3, 700, 128), (3, 50, 40000, 640),
     (5, 64, 51866, 1280), (5, 1, 51866, 1280), (5, 37, 20000, 384), (5, 64, 300, 64), (5, 5, 1000, 128),
-    (6, 1500, 1280, 1280), (6, 300, 200, 128), (6, 1500, 5120, 1280)])
+    (6, 1500, 1280, 1280), (6, 300, 200, 128), (6, 1500, 5120, 1280), (6, 1500, 1280, 5120),
+    (7, 1500, 1280, 1280), (7, 300, 200, 128)])
 def test_gemm_variants(eng, variant, M, N, K):
     rng = np.random.default_rng(M * 7 + N)
     A = rng.uniform(-1, 1, (M, K)).astype(np.float16)
@@ -37,7 +38,8 @@ def test_gemm_variants(eng, variant, M, N, K):
 
 @pytest.mark.parametrize("M,N,K", [(1500, 1280, 1280), (3000, 2304, 1280), (1500, 1280, 5120), (777, 264, 128)])
 def test_tile_sizes_bit_identical(eng, M, N, K):
-    """The encoder GEMM picks its tile by M (64 for one or a few windows, 128, or the
+    """The encoder GEMM picks its tile by M (64 for one or a few windows, with or without
+    the deep LDS ring, 128, or the
     8-phase 256 at large M): every output element is the same MFMA chain over K in the
     same order, so a window's encoder output does not depend on its batch."""
     rng = np.random.default_rng(M + N + K)
@@ -45,6 +47,8 @@ def test_tile_sizes_bit_identical(eng, M, N, K):
     W = rng.uniform(-1, 1, (N, K)).astype(np.float16)
     c1, _ = eng.debug_gemm(A, W, 1)
     c6, _ = eng.debug_gemm(A, W, 6)
+    c7, _ = eng.debug_gemm(A, W, 7)
     c4, _ = eng.debug_gemm(A, W, 4)
     assert np.array_equal(c1, c6)
+    assert np.array_equal(c1, c7)
     assert np.array_equal(c1, c4)

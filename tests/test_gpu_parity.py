@@ -168,6 +168,34 @@ def test_batch_equals_single(tiny_engine):
         assert one.language == together[i].language
 
 
+def test_decoder_step_forms_bit_identical():
+    """The three decoder-step forms give bit-identical logits for a window: 1 row (every
+    residual+LayerNorm and GELU reduce a GEMM prologue), 3 rows (GELU reduce as fc2's
+    prologue, resln.h GELU_ROWS) and 12 rows (every reduce its own kernel)."""
+    d = D.TINY_TEST
+    w = weights.random_weights(d, seed=1234, emb_std=0.5)
+    eng = WhisperEngine(d, device=0, max_batch=12)
+    try:
+        eng.load_weights(w)
+        sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+        cfg = DecodeConfig(suppress_tokens=sup, max_length=48)
+        pcm = synth.chirp_clip(13, 30.0)
+        got = {}
+        for n in (1, 3, 12):
+            eng.log_mel([pcm] * n)
+            eng.encode([(i, 0, 3000) for i in range(n)])
+            outs = eng.decode(n, cfg, dump_steps=6)
+            for o in outs:
+                assert o.tokens == outs[0].tokens
+            got[n] = outs[-1]
+        for n in (3, 12):
+            assert got[n].tokens == got[1].tokens
+            for i in range(len(got[1].logits)):
+                np.testing.assert_array_equal(got[n].logits[i], got[1].logits[i], err_msg=f"rows {n} step {i}")
+    finally:
+        eng.close()
+
+
 def test_turbo_encoder_layer_matches_golden():
     z = np.load(os.path.join(GOLD, "turbo_enc_layer0.npz"))
     d = D.LARGE_V3_TURBO

@@ -4,8 +4,8 @@ set -e
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/${1:-lat}; mkdir -p $O
 AB=${2:-OSW_NONE=1}
-if [ -n "$3" ]; then K="-k $3"; else K=""; fi
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread $K > $O/gpu_tests.log 2>&1
+if [ -n "$3" ]; then K=(-k "$3"); else K=(); fi
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread "${K[@]}" > $O/gpu_tests.log 2>&1
 for beam in 1 5; do
   timeout -k 10 120 python -u tools/latency_probe.py 20 $beam > $O/lat_a_beam$beam.txt 2>&1
   env $AB timeout -k 10 120 python -u tools/latency_probe.py 20 $beam > $O/lat_b_beam$beam.txt 2>&1

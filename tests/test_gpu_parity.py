@@ -339,6 +339,40 @@ def test_sibling_beam_concurrent_is_deterministic(tiny_engine):
         sib.close()
 
 
+def test_mel_bit_identical_under_concurrent_encoder(tiny_engine):
+    """The log-mel of a context is bit-identical while a sibling context's encoder runs on
+    its own stream.  A build with packed-FP32 VALU ops fails this in 6-10 of 16 calls (the
+    last 16 lanes of the DFT's second stage); the library is built without
+    them."""
+    import threading
+    d, eng, w = tiny_engine
+    sib = eng.sibling(max_batch=2)
+    try:
+        clips = [synth.chirp_clip(31, 30.0), synth.chirp_clip(32, 11.0)]
+        wins = [(0, 0, 3000), (1, 0, 1099)]
+        sib.log_mel(clips)
+        ref = [sib.get_mel(i).copy() for i in range(2)]
+        eng.log_mel(clips)
+        eng.encode(wins)
+        stop = []
+
+        def loop():
+            while not stop:
+                eng.encode(wins)
+        t = threading.Thread(target=loop)
+        t.start()
+        try:
+            for _ in range(16):
+                sib.log_mel(clips)
+                for i in range(2):
+                    np.testing.assert_array_equal(sib.get_mel(i), ref[i])
+        finally:
+            stop.append(1)
+            t.join()
+    finally:
+        sib.close()
+
+
 def test_sampling_draws_match_oracle(tiny_engine):
     """temperature > 0: every pick is argmax(x / T + Gumbel(seed, row, step, token)) over
     the rule-masked logits.  Replayed by the oracle on the GPU's own logits: ids exact;

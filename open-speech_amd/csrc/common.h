@@ -133,7 +133,8 @@ __device__ __forceinline__ void split_h16(float v, h16* hi, h16* lo, int64_t i) 
 // launchers (defined in the .hip files)
 void launch_gemm(const GemmArgs& g, hipStream_t s);
 void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s);  // 0 auto, 1 128-tile, 2 256-tile,
-                                                                          // 4 8-phase 256, 5 wide, 6 64-tile ring, 7 64-tile
+                                                                          // 4 8-phase 256, 5 wide, 6 64-tile ring, 7 64-tile;
+                                                                          // debug: 8 8-phase fp16 out, 9 no epilogue, 10 GELU
 // M <= 64, K % 128 == 0; `part` needs skinny_ksplit(N,K)*M*N floats
 void launch_gemm_skinny(const GemmArgs& g, float* part, hipStream_t s);
 int skinny_ksplit(int N, int K);

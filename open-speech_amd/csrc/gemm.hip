@@ -413,7 +413,7 @@ void launch256(const GemmArgs& g0, hipStream_t s) {
 // drained inside the loop (raw s_barrier, no __syncthreads).
 constexpr int HT = 128 * BK;  // halfs per half-tile
 
-template <int EPI>
+template <int EPI, bool NOEPI = false>  // NOEPI: no epilogue (debug variant 9: main-loop time alone)
 __global__ __launch_bounds__(GNT, 1) void gemm8p_kernel(GemmArgs g) {
     extern __shared__ __attribute__((aligned(16))) h16 smem[];  // [2][A0 A1 W0 W1][128*64]
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -545,21 +545,31 @@ __global__ __launch_bounds__(GNT, 1) void gemm8p_kernel(GemmArgs g) {
         barrier();
     }
     if (__builtin_amdgcn_readfirstlane(wave) < 4) barrier();
-    staged_epilogue<EPI, true>(g, acc, m0, n0, wm, wn, (char*)smem);
+    if constexpr (NOEPI) {
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+        if (t == 1234.5f) ((float*)g.C)[threadIdx.x] = t;  // keeps the loop live
+    } else {
+        staged_epilogue<EPI, true>(g, acc, m0, n0, wm, wn, (char*)smem);
+    }
 }
 
-template <int EPI>
+template <int EPI, bool NOEPI = false>
 void launch8p(const GemmArgs& g0, hipStream_t s) {
     static bool attr = false;
     constexpr int lds = EPI_LDS > 8 * HT * 2 ? EPI_LDS : 8 * HT * 2;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gemm8p_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        (void)hipFuncSetAttribute((const void*)gemm8p_kernel<EPI, NOEPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  lds);
         attr = true;
     }
     GemmArgs g = g0;
     g.band = choose_band(g);
     const int nwg = ((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
-    gemm8p_kernel<EPI><<<nwg, GNT, lds, s>>>(g);
+    gemm8p_kernel<EPI, NOEPI><<<nwg, GNT, lds, s>>>(g);
 }
 
 
@@ -1164,6 +1174,18 @@ void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s) {
                                                    !getenv("OSW_GEMM128")));
 
     static const bool two_phase = getenv("OSW_GEMM_2PHASE") != nullptr;  // A/B switch for the 8-phase schedule
+    if (variant == 8) {  // debug: 8-phase, fp16 out / GELU fp16 out / no epilogue
+        launch8p<EPI_F16>(g, s);
+        return;
+    }
+    if (variant == 9) {
+        launch8p<EPI_F32, true>(g, s);
+        return;
+    }
+    if (variant == 10) {
+        launch8p<EPI_F16_GELU>(g, s);
+        return;
+    }
     if (variant == 4 || (variant == 0 && big && !two_phase)) {
         switch (g.epi) {
             case EPI_F16: launch8p<EPI_F16>(g, s); return;

@@ -216,13 +216,20 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
     const int lane = threadIdx.x & 63, tid = threadIdx.x;
     __syncthreads();
     if constexpr (EPI == EPI_F16 || EPI == EPI_F16_GELU || EPI == EPI_HEADS) {
+        // IL (every wave holds rows of both 128-row halves): the tile leaves in two halves,
+        // so the second half's bias/GELU (VALU) runs while the first half's stores drain
+        // (the whole grid reaches its epilogue together: the stores are HBM-bound there)
         h16* T = (h16*)smem;
+        constexpr int NH = IL ? 2 : 1;
+#pragma unroll
+        for (int half = 0; half < NH; ++half) {
 #pragma unroll
         for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
+                    if (IL && (mi >> 2) != half) continue;
                     const int row = acc_row<IL>(wm, mi) + (lane >> 4) * 4 + i;
                     const int col = acc_col<IL>(wn, ni) + (lane & 15);
                     const int n = min(n0 + col, g.N - 1);
@@ -230,9 +237,9 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
                 }
         __syncthreads();
 #pragma unroll 4
-        for (int j = 0; j < 16; ++j) {
+        for (int j = 0; j < 16 / NH; ++j) {
             const int id = j * GNT + tid;
-            const int row = id >> 5, c8 = (id & 31) * 8;
+            const int row = half * 128 + (id >> 5), c8 = (id & 31) * 8;
             const int m = m0 + row, n = n0 + c8;
             if (m >= g.M || n >= g.N) continue;
             const h16x8 v = *(const h16x8*)&T[row * EP16 + c8];
@@ -246,6 +253,7 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
                 dst = (h16*)g.C + (m / g.c_grp_rows) * g.c_grp_stride + (int64_t)(m % g.c_grp_rows) * g.ldc + n;
             }
             __builtin_nontemporal_store(v, (h16x8*)dst);
+        }
         }
     } else {
         float* T = (float*)smem;

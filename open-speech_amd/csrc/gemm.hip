@@ -185,13 +185,18 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
 constexpr int GB = 256, GNT = 512;
 
 // LDS-staged epilogue for the 256x256 tile: the accumulators (bias / GELU / pos
-// applied) are written to an LDS image of the tile (rows padded so the MFMA-layout
-// writes are conflict-free), then every thread streams 16-B chunks to global —
-// 1 KiB contiguous per wave-instruction instead of 128 scattered 2/4-B stores per
-// lane.  fp32 tiles go through LDS in two 128-row halves.
-constexpr int EP16 = 264;  // fp16 row stride (halfs)
-constexpr int EP32 = 260;  // fp32 row stride (floats)
-constexpr int EPI_LDS = 256 * EP16 * 2;  // 135168 B >= 128 * EP32 * 4
+// applied) are written to an LDS image of the tile, then every thread streams 16-B
+// chunks to global — 1 KiB contiguous per wave-instruction instead of 128 scattered
+// 2/4-B stores per lane.  fp32 tiles go through LDS in two 128-row halves.  The image
+// rows are unpadded with the 16-B chunk XOR-swizzled by row (conflict-free MFMA-layout
+// writes: the 4 rows of one write are 4 apart, so their chunks land on distinct banks),
+// so the image is exactly the 128 KiB operand ring: the kernel leaves 32 KiB of the
+// CU's LDS free, enough for a co-resident decoder workgroup of another lane (a padded
+// 135 KiB image left 28 KiB, which no skinny GEMM workgroup fits: the decoder's
+// projections then waited for whole encoder tiles to retire).
+constexpr int EPI_LDS = 256 * 256 * 2;  // 131072 B = 128 rows x 256 fp32
+__device__ __forceinline__ int ep16(int row, int col) { return row * 256 + ((((col >> 3) ^ row) & 31) << 3) + (col & 7); }
+__device__ __forceinline__ int ep32(int row, int col) { return row * 256 + ((((col >> 2) ^ row) & 63) << 2) + (col & 3); }
 
 template <int EPI>
 __device__ __forceinline__ float epi_value(const GemmArgs& g, int m, int n, float v) {
@@ -233,7 +238,7 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
                     const int row = acc_row<IL>(wm, mi) + (lane >> 4) * 4 + i;
                     const int col = acc_col<IL>(wn, ni) + (lane & 15);
                     const int n = min(n0 + col, g.N - 1);
-                    T[row * EP16 + col] = (h16)epi_value<EPI>(g, m0 + row, n, acc[mi][ni][i]);
+                    T[ep16(row, col)] = (h16)epi_value<EPI>(g, m0 + row, n, acc[mi][ni][i]);
                 }
         __syncthreads();
 #pragma unroll 4
@@ -242,7 +247,7 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
             const int row = half * 128 + (id >> 5), c8 = (id & 31) * 8;
             const int m = m0 + row, n = n0 + c8;
             if (m >= g.M || n >= g.N) continue;
-            const h16x8 v = *(const h16x8*)&T[row * EP16 + c8];
+            const h16x8 v = *(const h16x8*)&T[ep16(row, c8)];
             h16* dst;
             if constexpr (EPI == EPI_HEADS) {
                 const int D = g.heads_H * 64;
@@ -269,7 +274,7 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
                             const int row = acc_row<IL>(wm, mi) - half * 128 + (lane >> 4) * 4 + i;
                             const int col = acc_col<IL>(wn, ni) + (lane & 15);
                             const int n = min(n0 + col, g.N - 1);
-                            T[row * EP32 + col] = epi_value<EPI>(g, m0 + half * 128 + row, n, acc[mi][ni][i]);
+                            T[ep32(row, col)] = epi_value<EPI>(g, m0 + half * 128 + row, n, acc[mi][ni][i]);
                         }
             }
             __syncthreads();
@@ -279,7 +284,7 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
                 const int row = id >> 6, c4 = (id & 63) * 4;
                 const int m = m0 + half * 128 + row, n = n0 + c4;
                 if (m < g.M && n < g.N) {
-                    f32x4 v = *(const f32x4*)&T[row * EP32 + c4];
+                    f32x4 v = *(const f32x4*)&T[ep32(row, c4)];
                     float* dst = (float*)g.C + (m / g.c_grp_rows) * g.c_grp_stride +
                                  (int64_t)(m % g.c_grp_rows) * g.ldc + n;
                     if constexpr (EPI == EPI_F32_RESID) v += *(const f32x4*)dst;
@@ -709,10 +714,13 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
     // or the GELU reduce of this workgroup's K range (PRO_GELU).  The MFMA order is the
     // plain kernel's, so both paths give identical results.
     static_assert(PRO == PRO_NONE || (MT == 1 && LO), "the prologue serves <= 8 hi/lo rows");
-    constexpr int CK = (LO && MT > 2) ? 4 : 8;  // k32 steps per chunk
+    // k32 steps per chunk; 64 hi/lo rows use 64-deep chunks: the two A buffers are then
+    // 32 KiB, so a workgroup fits beside another lane's encoder GEMM (staged_epilogue)
+    constexpr int CK = (LO && MT > 2) ? 2 : 8;
     constexpr int CKK = CK * 32;                 // k per chunk
     constexpr int CPR = CKK / 8;                 // 16-B pieces of one row per chunk
     constexpr int RPP = 64 / CPR;                // rows per 1-KiB glds wave-instruction
+    constexpr int SWM = (CPR < 16 ? CPR : 16) - 1;  // XOR swizzle of the 16-B chunk by row, within the row
     constexpr int ROWS = MT * 16;
     constexpr int NIMG = LO ? 2 : 1;
     constexpr int APIECES = ROWS / RPP / 4;      // glds per wave per image per chunk
@@ -737,7 +745,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
     for (int i = 0; i < APIECES; ++i) {
         const int j = i * 4 + wave;
         const int row = RPP * j + lane / CPR;
-        acl[i] = ((lane % CPR) ^ (row & 15)) * 8;
+        acl[i] = ((lane % CPR) ^ (row & SWM)) * 8;
         const int64_t gr = min(mb + row, g.M - 1);
         asrc[0][i] = grp_row(g.A, gr, g.a_grp_rows, g.a_grp_stride, g.lda) + k0;
         if constexpr (LO) asrc[NIMG - 1][i] = grp_row(g.A_lo, gr, g.a_grp_rows, g.a_grp_stride, g.lda) + k0;
@@ -788,7 +796,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
                     af = *(const h16x8*)&Ap[0][r][kk];
                     al = *(const h16x8*)&Ap[PRO ? 1 : 0][r][kk];
                 } else {
-                    const int ch = ((u + shift) * 4 + gq) ^ (row & 15);
+                    const int ch = ((u + shift) * 4 + gq) ^ (row & SWM);
                     af = *(const h16x8*)&As[buf][0][row * CKK + ch * 8];
                     if constexpr (LO) al = *(const h16x8*)&As[buf][NIMG - 1][row * CKK + ch * 8];
                 }

@@ -68,7 +68,7 @@ __global__ void dec_embed_kernel(const h16* __restrict__ tok_emb, const float* _
                                  const int* __restrict__ tok, const int* __restrict__ pos_ptr, int D, int ctx,
                                  float* __restrict__ x) {
     const int b = blockIdx.x;
-    const int t = tok[b];
+    const int t = max(tok[b], 0);  // an invalid id (a NaN row's select) must not fault
     const int pos = min(*pos_ptr, ctx - 1);
     for (int c = threadIdx.x; c < D; c += blockDim.x)
         x[(int64_t)b * D + c] = (float)tok_emb[(int64_t)t * D + c] + pos_emb[(int64_t)pos * D + c];

@@ -714,9 +714,10 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
     // or the GELU reduce of this workgroup's K range (PRO_GELU).  The MFMA order is the
     // plain kernel's, so both paths give identical results.
     static_assert(PRO == PRO_NONE || (MT == 1 && LO), "the prologue serves <= 8 hi/lo rows");
-    // k32 steps per chunk; 64 hi/lo rows use 64-deep chunks: the two A buffers are then
-    // 32 KiB, so a workgroup fits beside another lane's encoder GEMM (staged_epilogue)
-    constexpr int CK = (LO && MT > 2) ? 2 : 8;
+    // k32 steps per chunk; >= 32 hi/lo rows use 64-deep chunks: the two A buffers of 32
+    // rows are then 16 KiB, so a workgroup fits beside another lane's encoder GEMM
+    // workgroup (which leaves 30 KiB of the CU's LDS free, tools/coresidency_probe.hip)
+    constexpr int CK = (LO && MT >= 2) ? 2 : 8;
     constexpr int CKK = CK * 32;                 // k per chunk
     constexpr int CPR = CKK / 8;                 // 16-B pieces of one row per chunk
     constexpr int RPP = 64 / CPR;                // rows per 1-KiB glds wave-instruction
@@ -1094,16 +1095,20 @@ int skinny_ksplit(int N, int K) {
 // partial-slab mode: always writes part[ks][M][N] (no epilogue); returns ksplit.
 // M > 64 (beam rows) runs ceil(M / 64) row groups on grid z; they read the same
 // weights, so the weight stream comes from HBM once and from the MALL/L2 after.
+// Hi/lo rows beyond 32 run as 32-row groups (MT = 2, 16 KiB of LDS): a 64-row workgroup
+// (32 KiB) cannot start beside another lane's encoder GEMM tile, and the decoder then
+// stalled for whole encoder tiles (51 us per projection instead of 16).
 int launch_gemm_skinny_partial(const GemmArgs& g, float* part, hipStream_t s) {
     const int ks = skinny_ksplit(g.N, g.K);
-    const dim3 grid((g.N + 63) / 64, ks, (g.M + 63) / 64);
+    const int gr = (g.A_lo && g.M > 32) ? 32 : 64;
+    const dim3 grid((g.N + 63) / 64, ks, (g.M + gr - 1) / gr);
     const int kc = g.K / ks;
 #define OSW_SKINNY_PART(MT_)                                                                     \
     do {                                                                                         \
         if (g.A_lo) gemm_skinny_kernel<MT_, false, EPI_F32, true><<<grid, 256, 0, s>>>(g, kc, part, ProArgs{}); \
         else gemm_skinny_kernel<MT_, false, EPI_F32, false><<<grid, 256, 0, s>>>(g, kc, part, ProArgs{}); \
     } while (0)
-    switch (std::min(g.M, 64) <= 16 ? 1 : std::min(g.M, 64) <= 32 ? 2 : std::min(g.M, 64) <= 48 ? 3 : 4) {
+    switch (std::min(g.M, gr) <= 16 ? 1 : std::min(g.M, gr) <= 32 ? 2 : std::min(g.M, gr) <= 48 ? 3 : 4) {
         case 1: OSW_SKINNY_PART(1); break;
         case 2: OSW_SKINNY_PART(2); break;
         case 3: OSW_SKINNY_PART(3); break;

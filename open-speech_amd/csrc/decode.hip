@@ -829,6 +829,7 @@ __device__ __forceinline__ SelPart load_part(const SelPart* src) {
 }
 
 // grid (B, SEL_SPLIT), 256 threads: one vocabulary slice of one row
+template <bool SAMPLE>
 __device__ __forceinline__ void select_partial_body(const float* __restrict__ logits, const SelParams& P, int step,
                                                     const unsigned* __restrict__ supmask,
                                                     const SelState* __restrict__ st, SelPart* __restrict__ parts) {
@@ -842,7 +843,7 @@ __device__ __forceinline__ void select_partial_body(const float* __restrict__ lo
     const RowRules R = row_rules(P, s);
     float m_all = -INFINITY, s_all = 0.f, m_ts = -INFINITY, s_ts = 0.f;
     ArgMax a_all{-INFINITY, 0x7fffffff}, a_text{-INFINITY, 0x7fffffff}, a_ts{-INFINITY, 0x7fffffff};
-    const unsigned long long seed = P.inv_temp > 0.f ? *P.seed : 0ull;
+    const unsigned long long seed = SAMPLE ? *P.seed : 0ull;
     // the thread's entries v = lo + tid + 256 i in order, their logits and suppress words
     // loaded 8 at a time (clamped addresses) before any is used: one memory round trip per
     // 8 entries instead of one per entry (batch 1: 18 -> 8 us per step)
@@ -870,7 +871,7 @@ __device__ __forceinline__ void select_partial_body(const float* __restrict__ lo
             lse_add(m_all, s_all, xv);
             // sampling: a_all / a_ts pick the Gumbel-perturbed maximum; a_text stays the plain
             // maximum (the timestamp-mass rule compares against it)
-            const float key = P.inv_temp > 0.f ? xv * P.inv_temp + gumbel_noise(seed, b, step, v) : xv;
+            const float key = SAMPLE ? xv * P.inv_temp + gumbel_noise(seed, b, step, v) : xv;
             a_all = amax(a_all, ArgMax{key, v});
             if (v >= P.tb) {
                 lse_add(m_ts, s_ts, xv);
@@ -913,6 +914,9 @@ __device__ __forceinline__ void select_partial_body(const float* __restrict__ lo
 template <bool DEVICE>
 __device__ __forceinline__ SelPart combine_parts(const SelPart* __restrict__ parts) {
     SelPart r = DEVICE ? load_part(parts) : parts[0];
+    // partly unrolled: fully unrolled, the 15 parts' loads were hoisted together and the
+    // select kernel held 112 VGPRs for this one-thread tail
+#pragma unroll 4
     for (int i = 1; i < SEL_SPLIT; ++i) {
         const SelPart q = DEVICE ? load_part(parts + i) : parts[i];
         lse_merge(r.m_all, r.s_all, q.m_all, q.s_all);
@@ -1126,6 +1130,10 @@ __device__ __forceinline__ void beam_slice_body(const float* __restrict__ logits
 // slices in fixed order and picks the row's token (select_final_row).  With `bump`
 // (greedy steps) the last row to be finalised advances the device step counter: by
 // then every slice of every row has read it.  One launch instead of partial + final.
+// MODE 0: greedy rows, 1: sampling rows (temperature > 0), 2: beam rows.  Each launch
+// compiles only its own path: the greedy kernel carries neither the Gumbel keys nor the
+// beam candidate lists (112 -> fewer VGPRs, so it can sit beside another lane's encoder).
+template <int MODE>
 __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ logits, SelParams P,
                                                      int* __restrict__ pos_ptr, const unsigned* __restrict__ supmask,
                                                      const int* __restrict__ prompt, SelPart* __restrict__ parts,
@@ -1134,7 +1142,7 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ l
                                                      int* __restrict__ arrive, int* __restrict__ ticket, int bump,
                                                      BeamCand* __restrict__ cand) {
     const int step = *pos_ptr;
-    if (P.beam > 1) {
+    if (MODE == 2 && P.beam > 1) {
         const SelState s = st[blockIdx.x];
         if (sel_mode(P, step, s) == SEL_SAMPLE) {  // the same for every slice of the row
             // beam rows' sampling steps: statistics + candidates in one pass; nothing to
@@ -1144,7 +1152,7 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ l
             return;
         }
     }
-    select_partial_body(logits, P, step, supmask, st, parts);
+    select_partial_body<MODE == 1>(logits, P, step, supmask, st, parts);
     __shared__ int last;
     __shared__ SelPart rp[SEL_SPLIT];
     const int b = blockIdx.x;
@@ -1458,9 +1466,16 @@ void launch_select(const float* logits, int rows, int* pos, const SelParams& P, 
                    int* arrive, bool bump, void* cand, hipStream_t s) {
     // arrive[0]: rows finalised this step; arrive[1 + row]: the row's slice tickets; cand:
     // the beam rows' candidate lists (beam_slice_body)
-    select_kernel<<<dim3(rows, SEL_SPLIT), 256, 0, s>>>(logits, P, pos, supmask, prompt, (SelPart*)sel_parts, st,
-                                                        cur_tok, tokens, max_tokens, arrive, arrive + 1, bump ? 1 : 0,
-                                                        (BeamCand*)cand);
+    const dim3 grid(rows, SEL_SPLIT);
+    if (P.beam > 1)
+        select_kernel<2><<<grid, 256, 0, s>>>(logits, P, pos, supmask, prompt, (SelPart*)sel_parts, st, cur_tok, tokens,
+                                               max_tokens, arrive, arrive + 1, bump ? 1 : 0, (BeamCand*)cand);
+    else if (P.inv_temp > 0.f)
+        select_kernel<1><<<grid, 256, 0, s>>>(logits, P, pos, supmask, prompt, (SelPart*)sel_parts, st, cur_tok, tokens,
+                                               max_tokens, arrive, arrive + 1, bump ? 1 : 0, (BeamCand*)cand);
+    else
+        select_kernel<0><<<grid, 256, 0, s>>>(logits, P, pos, supmask, prompt, (SelPart*)sel_parts, st, cur_tok, tokens,
+                                               max_tokens, arrive, arrive + 1, bump ? 1 : 0, (BeamCand*)cand);
 }
 
 void launch_beam(const float* logits, int windows, int* pos, const SelParams& P, const unsigned* supmask,

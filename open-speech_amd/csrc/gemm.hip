@@ -217,8 +217,8 @@ __device__ __forceinline__ int acc_col(int wn, int ni) { return IL ? (ni >> 1) *
 // next GEMM's operand panels (8p GEMMs 4-7 % and the attention after them 6 % faster).
 template <int EPI, bool IL = false>
 __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], int m0, int n0, int wm,
-                                                int wn, char* smem) {
-    const int lane = threadIdx.x & 63, tid = threadIdx.x;
+                                                int wn, char* smem, int tid) {
+    const int lane = tid & 63;
     __syncthreads();
     if constexpr (EPI == EPI_F16 || EPI == EPI_F16_GELU || EPI == EPI_HEADS) {
         // IL (every wave holds rows of both 128-row halves): the tile leaves in two halves,
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(GNT, 1) void gemm256_kernel(GemmArgs g) {
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
     }
-    staged_epilogue<EPI>(g, acc, m0, n0, wm, wn, (char*)smem);
+    staged_epilogue<EPI>(g, acc, m0, n0, wm, wn, (char*)smem, threadIdx.x);
 }
 
 // band width minimising modelled L2-miss bytes: A re-read once per band, a band's
@@ -426,13 +426,11 @@ void launch256(const GemmArgs& g0, hipStream_t s) {
 // drained inside the loop (raw s_barrier, no __syncthreads).
 constexpr int HT = 128 * BK;  // halfs per half-tile
 
-template <int EPI, bool NOEPI = false>  // NOEPI: no epilogue (debug variant 9: main-loop time alone)
-__global__ __launch_bounds__(GNT, 1) void gemm8p_kernel(GemmArgs g) {
-    extern __shared__ __attribute__((aligned(16))) h16 smem[];  // [2][A0 A1 W0 W1][128*64]
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+template <int EPI, bool NOEPI>
+__device__ __forceinline__ void gemm8p_tile(const GemmArgs& g, int bid, h16* smem, int tid) {
+    const int wave = tid >> 6, lane = tid & 63;
     const int ntn = (g.N + GB - 1) / GB, ntm = (g.M + GB - 1) / GB;
     const int nwg = ntn * ntm;
-    const int bid = blockIdx.x;
     const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
     const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
     const int G = g.band > 0 ? min(g.band, ntn) : ntn;
@@ -564,9 +562,32 @@ __global__ __launch_bounds__(GNT, 1) void gemm8p_kernel(GemmArgs g) {
         for (int i = 0; i < 8; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
-        if (t == 1234.5f) ((float*)g.C)[threadIdx.x] = t;  // keeps the loop live
+        if (t == 1234.5f) ((float*)g.C)[tid] = t;  // keeps the loop live
     } else {
-        staged_epilogue<EPI, true>(g, acc, m0, n0, wm, wn, (char*)smem);
+        staged_epilogue<EPI, true>(g, acc, m0, n0, wm, wn, (char*)smem, tid);
+    }
+}
+
+// Persistent (launch8p; OSW_GEMM_PERSIST=0: one workgroup per tile): one workgroup per CU
+// looping over tiles — workgroup b runs
+// virtual ids b, b + grid, ... (grid a multiple of 8, so every id of a workgroup maps to its
+// own XCD's contiguous tile run, as in the one-tile-per-workgroup grid).  No encoder
+// workgroups then wait in the dispatcher, where they delayed another lane's decoder
+// dispatches by 17-30 us each; every decoder kernel of a greedy step must
+// then fit beside an encoder workgroup (<= 30 KiB of LDS, <= 80 VGPRs); the 64-row logits
+// GEMM (80 KiB) does not.  4832 vs 4789 audio-s/s (12 steps, two runs each).
+template <int EPI, bool NOEPI = false>  // NOEPI: no epilogue (debug variant 9: main-loop time alone)
+__global__ __launch_bounds__(GNT, 1) void gemm8p_kernel(GemmArgs g) {
+    extern __shared__ __attribute__((aligned(16))) h16 smem[];  // [2][A0 A1 W0 W1][128*64]
+    const int nwg = ((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
+    for (int vb = blockIdx.x; vb < nwg; vb += gridDim.x) {
+        // the thread id passes through an opaque move each tile, so nothing derived from it
+        // (fragment offsets, staging addresses) is hoisted out of the loop and kept live
+        // across tiles: the one-tile body already needs ~206 VGPRs (hoisted: 256 + spills)
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        gemm8p_tile<EPI, NOEPI>(g, vb, smem, tid);
+        __syncthreads();  // the epilogue's LDS image is the next tile's operand ring
     }
 }
 
@@ -582,7 +603,15 @@ void launch8p(const GemmArgs& g0, hipStream_t s) {
     GemmArgs g = g0;
     g.band = choose_band(g);
     const int nwg = ((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
-    gemm8p_kernel<EPI, NOEPI><<<nwg, GNT, lds, s>>>(g);
+    static const int grid_cap = [] {
+        const char* e = std::getenv("OSW_GEMM_PERSIST");  // 0: one workgroup per tile
+        if (e && e[0] == '0') return 1 << 30;
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return 1 << 30;
+        return cus / 8 * 8;  // one workgroup per CU, a multiple of the 8 XCDs
+    }();
+    gemm8p_kernel<EPI, NOEPI><<<std::min(nwg, std::max(8, grid_cap)), GNT, lds, s>>>(g);
 }
 
 

@@ -1132,7 +1132,7 @@ __device__ __forceinline__ void beam_slice_body(const float* __restrict__ logits
 // then every slice of every row has read it.  One launch instead of partial + final.
 // MODE 0: greedy rows, 1: sampling rows (temperature > 0), 2: beam rows.  Each launch
 // compiles only its own path: the greedy kernel carries neither the Gumbel keys nor the
-// beam candidate lists (112 -> fewer VGPRs, so it can sit beside another lane's encoder).
+// beam candidate lists (47 VGPRs, so it fits beside another lane's encoder workgroup).
 template <int MODE>
 __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ logits, SelParams P,
                                                      int* __restrict__ pos_ptr, const unsigned* __restrict__ supmask,

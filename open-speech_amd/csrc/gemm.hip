@@ -569,9 +569,9 @@ __device__ __forceinline__ void gemm8p_tile(const GemmArgs& g, int bid, h16* sme
 }
 
 // Persistent (launch8p; OSW_GEMM_PERSIST=0: one workgroup per tile): one workgroup per CU
-// looping over tiles — workgroup b runs
-// virtual ids b, b + grid, ... (grid a multiple of 8, so every id of a workgroup maps to its
-// own XCD's contiguous tile run, as in the one-tile-per-workgroup grid).  No encoder
+// looping over tiles; workgroup b runs virtual ids b, b + grid, ... (grid a multiple of 8,
+// so every id of a workgroup maps to its own XCD's contiguous tile run, as in the
+// one-tile-per-workgroup grid).  No encoder
 // workgroups then wait in the dispatcher, where they delayed another lane's decoder
 // dispatches by 17-30 us each; every decoder kernel of a greedy step must
 // then fit beside an encoder workgroup (<= 30 KiB of LDS, <= 80 VGPRs); the 64-row logits

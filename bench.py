@@ -6,7 +6,9 @@ decode with Whisper's logits rules) over one batch of `--batch` synthetic 30 s
 16 kHz clips per GPU (BASELINE.json configs[2]; configs[3] is the same per-GPU shard
 at N=8).  With N>1 ranks (torchrun, one process per GPU) rank 0 holds every clip
 in HBM and the step starts with an RCCL scatter of the int16 PCM and ends with an
-RCCL gather of the token ids.
+RCCL gather of the token ids.  ``--gpus N`` alone starts the N
+ranks itself (torch.distributed.run on 127.0.0.1, before this process touches the
+GPU); under torchrun, WORLD_SIZE must equal ``--gpus`` or the bench exits non-zero.
 
 Prints ONE JSON line (rank 0).  value = audio seconds transcribed per wall second
 over all ranks (max-over-ranks time).  Weights are random (no checkpoint is
@@ -37,7 +39,7 @@ HBM_PEAK_GBS = 8000.0        # MI355X spec (MI355X_MICROARCH.md)
 MFMA_F16_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA spec
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=6)
@@ -68,7 +70,50 @@ def parse():
                          "<|endoftext|>: each clip's length is forced from a seeded distribution)")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r02_pmc.json"),
                     help="per-kernel HBM bytes from a rocprofv3 --pmc pass (tools/pmc_summary.py)")
-    return ap.parse_args()
+    ap.add_argument("--standin", action="store_true",
+                    help="launcher test only: ranks run a CPU stand-in engine over gloo (no GPU, no HIP library)")
+    return ap.parse_args(argv)
+
+
+def spawn_ranks(n: int, argv: list) -> int:
+    """``--gpus N`` (N > 1) outside a torchrun environment: start the N rank processes
+    here, one per GPU, as children of torch.distributed.run on 127.0.0.1, and return
+    their exit status.  Called before this process imports the HIP library or makes
+    any torch.cuda call (a process that has touched the GPU must not exec or hand its
+    device over).  Only rank 0 prints the JSON line, so the children's stdout is this
+    process's stdout."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+class StandInEngine:
+    """--standin: rank r takes (r + 1) x 40 ms per batch and decodes r + 1 tokens per
+    clip, so the launcher test sees the slow rank set the max-over-ranks time."""
+
+    def __init__(self, rank: int):
+        self.rank = rank
+
+    def transcribe_batch(self, clips, cfg, device_pcm=None, offsets=None):
+        class _Out:
+            tokens = list(range(self.rank + 1))
+        time.sleep(0.04 * (self.rank + 1))
+        return [_Out() for _ in clips]
+
+    def sibling(self):
+        return StandInEngine(self.rank)
+
+    def close(self):
+        pass
 
 
 def make_clips(n: int, offset: int = 0, unique: int = 32) -> np.ndarray:
@@ -237,44 +282,76 @@ def timed_steps(dp, allpcm, k: int, dist=None, dev=None):
     return el, ntok, res
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    if a.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        # one process per GPU: start the ranks ourselves (nothing here has touched the GPU)
+        sys.exit(spawn_ranks(a.gpus, argv))
+    world = int(env_world or "1")
+    if world != a.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}; launch one rank per GPU with matching counts")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
 
     dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if a.standin:
+        dev = torch.device("cpu")
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
     else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+        if world > 1:
+            import torch.distributed as dist
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.cuda.set_device(0)
+        dev = torch.device("cuda", local if world > 1 else 0)
     dims = D.PRESETS[a.model]
     B = a.batch
-    eng = WhisperEngine(dims, device=dev.index, max_batch=B)
-    eng.init_random(seed=0)
     sup = get_suppressed_tokens(WhisperTokenizer(dims.n_vocab), [-1])
     cfg = DecodeConfig(suppress_tokens=sup, max_length=a.max_length)
+    if a.standin:
+        eng = StandInEngine(rank)
+    else:
+        eng = WhisperEngine(dims, device=dev.index, max_batch=B)
+        eng.init_random(seed=0)
 
     n_total = B * world
     from open_speech_amd.distributed import DataParallelTranscriber
 
     dp = DataParallelTranscriber(eng, cfg, dist=dist, device=dev, clips_per_rank=B, ctx=dims.n_text_ctx,
-                                 lanes=a.lanes)
+                                 lanes=1 if a.standin else a.lanes)
     # inputs resident in HBM before timing: rank 0 holds every clip
     allpcm = torch.from_numpy(make_clips(n_total)).to(dev) if rank == 0 else None
 
     # warm-up: every lane captures its decode graph
     dp.run_steps(allpcm, max(a.warmup, len(dp.lanes)) if a.warmup > 0 else 0)
     el, ntok, res = timed_steps(dp, allpcm, a.steps, dist, dev)
-    profs = [e.profile() for e in dp.lanes]
 
     audio_s = n_total * a.steps * 30.0
     value = audio_s / el
     tokens_per_clip = ntok / (n_total * a.steps)
+    if a.standin:
+        if rank == 0:
+            print(json.dumps({
+                "metric": "audio-sec/sec (launcher test: CPU stand-in engine, not a measurement)",
+                "value": round(value, 2), "unit": "audio-sec/sec", "n_gpus": world, "steps": a.steps,
+                "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 2), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "none", "data": "stand-in engine over gloo",
+                "config": {"workload": "stand-in", "clips_per_gpu": B, "global_batch": n_total,
+                           "parallelism": f"dp{world}"},
+                "tokens_per_clip": round(tokens_per_clip, 3)}), flush=True)
+        dp.close()
+        if dist:
+            dist.destroy_process_group()
+        return
+    profs = [e.profile() for e in dp.lanes]
 
     # Realistic output lengths: real speech gives ~2-6 tokens per second of audio (text +
     # timestamp pairs), so each clip's greedy decode is cut at a length drawn from

@@ -142,6 +142,44 @@ def _bench_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _run_bench(args, env_extra=None, timeout=240):
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                               "MASTER_PORT")}
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd=ROOT)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p, [json.loads(ln) for ln in lines]
+
+
+def test_bench_gpus_flag_spawns_ranks():
+    """`bench.py --gpus 2` without a torchrun environment starts the two ranks itself
+    (BASELINE configs[3]'s launch): one JSON line, from rank 0, with n_gpus 2, the
+    global batch of both ranks, and the slow rank's time (max over ranks: rank 1 takes
+    80 ms per step in the stand-in)."""
+    p, lines = _run_bench(["--gpus", "2", "--standin", "--batch", "3", "--steps", "3", "--warmup", "1"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert len(lines) == 1, p.stdout
+    ln = lines[0]
+    assert ln["n_gpus"] == 2
+    assert ln["config"]["global_batch"] == 6 and ln["config"]["parallelism"] == "dp2"
+    assert ln["ms_per_step"] >= 80.0
+    assert ln["tokens_per_clip"] == 1.5            # rank 0 decodes 1 token per clip, rank 1 decodes 2
+    assert abs(ln["value"] - 6 * 3 * 30.0 / (ln["ms_per_step"] * 3 / 1e3)) / ln["value"] < 0.01
+
+
+def test_bench_world_size_mismatch_exits_nonzero():
+    """Under a launcher whose WORLD_SIZE disagrees with --gpus the bench refuses to run
+    rather than measure a different number of GPUs than it reports."""
+    p, lines = _run_bench(["--gpus", "4", "--standin"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"},
+                          timeout=120)
+    assert p.returncode != 0 and not lines
+    assert "WORLD_SIZE=2" in p.stderr
+
+
 def test_bench_accounting_gloo():
     """bench.py's timed region over ranks: the time is the MAX over ranks (the slow rank
     sets it) and tokens are summed over ranks, so `value` = all ranks' audio / that time."""

@@ -954,7 +954,15 @@ __device__ __forceinline__ void select_final_row(const float* __restrict__ logit
         const float* x = logits + (int64_t)b * P.V;
         s.nsp = __expf(x[P.no_speech] - lse_all);
         int next = prompt[b * P.prompt_len + step + 1];
-        if (next < 0) next = r.i_text;  // language detection: argmax over language tokens
+        if (next < 0) {
+            next = r.i_text;  // language detection: argmax over language tokens
+            // no language won (NaN logits: a NaN never beats the {-inf, INT_MAX} seed of
+            // amax): keep a valid token in the prompt and end the row, as beam_update does
+            if (next < P.first_lang || next >= P.first_lang + P.n_langs) {
+                next = P.first_lang;
+                s.done = 1;
+            }
+        }
         s.lang = next;
         st[b] = s;
         cur_tok[b] = next;
@@ -970,10 +978,15 @@ __device__ __forceinline__ void select_final_row(const float* __restrict__ logit
             lse = lse_ts;
         }
     }
+    // no candidate won (an all-NaN row keeps the amax seed's INT_MAX): the row ends with
+    // <|endoftext|> like beam_update's INT_MAX candidates, and nothing indexes with the id
+    const bool none = (unsigned)next >= (unsigned)P.V;
+    if (none) next = P.eot;
     // log-prob of the pick under the rule-masked, untempered distribution (what openai /
     // faster-whisper accumulate); sampling keys are perturbed, so read the logit back
-    float lp =
-        (P.inv_temp > 0.f ? logits[(int64_t)b * P.V + next] : (next == r.i_all ? r.v_all : r.v_ts)) - lse;
+    float lp = none ? logits[(int64_t)b * P.V + P.eot] - lse_all
+                    : (P.inv_temp > 0.f ? logits[(int64_t)b * P.V + next] : (next == r.i_all ? r.v_all : r.v_ts)) -
+                          lse;
     if (P.budget && P.budget[b] > 0 && n >= P.budget[b]) {  // length control: the row ends here
         next = P.eot;
         lp = logits[(int64_t)b * P.V + P.eot] - lse_all;
@@ -1449,8 +1462,8 @@ void launch_dec_cross_attn(const float* part, int ks, const float* bias, const h
 
 void launch_dec_resid_ln(const float* part, int ks, int B, int D, const float* bias, float* x, const float* g,
                          const float* be, h16* y, int64_t lo_off, const h16* tok_emb, const float* pos_emb,
-                         const int* tok, const int* pos, int ctx, hipStream_t s) {
-    ResLnArgs A{part, ks, (int64_t)B * D, bias, x, x, g, be, tok_emb, pos_emb, tok, pos, ctx, D};
+                         const int* tok, const int* pos, int ctx, int V, hipStream_t s) {
+    ResLnArgs A{part, ks, (int64_t)B * D, bias, x, x, g, be, tok_emb, pos_emb, tok, pos, ctx, D, V};
     dec_resid_ln_kernel<<<B, 256, 0, s>>>(A, y, lo_off);
 }
 

@@ -746,7 +746,10 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
     // k32 steps per chunk; >= 32 hi/lo rows use 64-deep chunks: the two A buffers of 32
     // rows are then 16 KiB, so a workgroup fits beside another lane's encoder GEMM
     // workgroup (which leaves 30 KiB of the CU's LDS free, tools/coresidency_probe.hip)
-    constexpr int CK = (LO && MT >= 2) ? 2 : 8;
+    // (48 hi/lo rows: 128-deep chunks, so the 4 waves' 1-KiB staging pieces cover all 48
+    // rows; a 64-deep chunk stages 32 rows per round and would leave rows 32-47 unstaged.
+    // Not reachable from the launchers, which group hi/lo rows by 32; kept valid anyway.)
+    constexpr int CK = (LO && MT >= 2) ? (MT == 3 ? 4 : 2) : 8;
     constexpr int CKK = CK * 32;                 // k per chunk
     constexpr int CPR = CKK / 8;                 // 16-B pieces of one row per chunk
     constexpr int RPP = 64 / CPR;                // rows per 1-KiB glds wave-instruction
@@ -754,6 +757,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
     constexpr int ROWS = MT * 16;
     constexpr int NIMG = LO ? 2 : 1;
     constexpr int APIECES = ROWS / RPP / 4;      // glds per wave per image per chunk
+    static_assert(PRO != PRO_NONE || APIECES * 4 * RPP == ROWS, "the staging pieces cover every row exactly once");
     __shared__ __attribute__((aligned(16))) h16 As[PRO ? 1 : 2][NIMG][PRO ? 8 : ROWS * CKK];
     constexpr int APR = PRO == PRO_GELU ? GELU_ROWS : PRO == PRO_RESLN ? PRO_ROWS : 1;  // image rows
     constexpr int APS = PRO == PRO_GELU ? GELU_KC + 8 : PRO == PRO_RESLN ? PRO_STRIDE : 8;

@@ -63,17 +63,6 @@ __global__ void init_uniform_kernel(T* dst, int64_t n, uint64_t key, float scale
     }
 }
 
-// x[b][:] = tok_emb[tok[b]] + pos_emb[pos]   (fp32 residual stream of the decoder)
-__global__ void dec_embed_kernel(const h16* __restrict__ tok_emb, const float* __restrict__ pos_emb,
-                                 const int* __restrict__ tok, const int* __restrict__ pos_ptr, int D, int ctx,
-                                 float* __restrict__ x) {
-    const int b = blockIdx.x;
-    const int t = max(tok[b], 0);  // an invalid id (a NaN row's select) must not fault
-    const int pos = min(*pos_ptr, ctx - 1);
-    for (int c = threadIdx.x; c < D; c += blockDim.x)
-        x[(int64_t)b * D + c] = (float)tok_emb[(int64_t)t * D + c] + pos_emb[(int64_t)pos * D + c];
-}
-
 __global__ void f16_to_f32_kernel(const h16* __restrict__ a, float* __restrict__ b, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         b[i] = (float)a[i];
@@ -111,10 +100,6 @@ void launch_init_uniform(void* dst, bool is_f16, int64_t n, uint64_t key, float 
         init_uniform_kernel<float><<<blocks, 256, 0, s>>>((float*)dst, n, key, scale, offset, zlo, zhi);
 }
 
-void launch_dec_embed(const h16* tok_emb, const float* pos_emb, const int* tok, const int* pos, int B, int D, int ctx,
-                      float* x, hipStream_t s) {
-    dec_embed_kernel<<<B, 256, 0, s>>>(tok_emb, pos_emb, tok, pos, D, ctx, x);
-}
 
 void launch_f16_to_f32(const h16* a, float* b, int64_t n, hipStream_t s) {
     f16_to_f32_kernel<<<1024, 256, 0, s>>>(a, b, n);

@@ -33,13 +33,12 @@ void launch_mel_normalize(const float*, int64_t, int, int, const int*, int, floa
 void launch_enc_attn(const h16*, h16*, int, int, int, hipStream_t);
 void launch_init_uniform(void*, bool, int64_t, uint64_t, float, float, int64_t, int64_t, hipStream_t);
 uint64_t hash_stream_key(uint64_t, int64_t);
-void launch_dec_embed(const h16*, const float*, const int*, const int*, int, int, int, float*, hipStream_t);
 void launch_dec_self_attn(const float*, int, const float*, h16*, h16*, const int*, int, int, int, h16*, int64_t,
                           const int*, int, const SelState*, hipStream_t);
 void launch_dec_cross_attn(const float*, int, const float*, const h16*, const h16*, int, int, int, int, h16*, int64_t,
                            float*, int*, const SelState*, hipStream_t);
 void launch_dec_resid_ln(const float*, int, int, int, const float*, float*, const float*, const float*, h16*, int64_t,
-                         const h16*, const float*, const int*, const int*, int, hipStream_t);
+                         const h16*, const float*, const int*, const int*, int, int, hipStream_t);
 void launch_dec_reduce_gelu(const float*, int, int, int, const float*, h16*, int64_t, hipStream_t);
 void launch_ingest_sumsq(const int16_t*, int, int, const int2*, int, float*, float*, hipStream_t);
 void launch_ingest_gain(const int16_t*, int64_t, int, int, float, int16_t*, hipStream_t);
@@ -102,6 +101,36 @@ T* dalloc(size_t n, std::vector<void*>& owned) {
     owned.push_back(p);
     return (T*)p;
 }
+
+// Frees a buffer dalloc'd into `owned` (implicitly synchronises the device; growth only).
+template <typename T>
+void dfree(T*& p, std::vector<void*>& owned) {
+    if (!p) return;
+    for (auto it = owned.begin(); it != owned.end(); ++it)
+        if (*it == (void*)p) {
+            owned.erase(it);
+            break;
+        }
+    (void)hipFree(p);
+    p = nullptr;
+}
+
+// Makes `device` current for one C-ABI call and restores the caller's device after it:
+// a host thread that calls into the library and then issues its own HIP / torch work
+// stays on the GPU it was on.
+struct DeviceScope {
+    int prev = -1;
+    explicit DeviceScope(int device) {
+        HIPCHK(hipGetDevice(&prev));
+        if (prev != device) HIPCHK(hipSetDevice(device));
+    }
+    ~DeviceScope() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+    DeviceScope(const DeviceScope&) = delete;
+    DeviceScope& operator=(const DeviceScope&) = delete;
+};
 
 struct EventPair {
     hipEvent_t a, b;
@@ -340,8 +369,11 @@ void build_weight_table(osw_ctx* c) {
         throw OswError(OSW_ENOMEM, "hipMalloc " + std::to_string(total) + " B (weights) failed");
     const int dev = c->device;
     c->arena = std::shared_ptr<void>(ap, [dev](void* p) {
+        int prev = -1;
+        (void)hipGetDevice(&prev);
         (void)hipSetDevice(dev);
         (void)hipFree(p);
+        if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
     });
     char* arena = (char*)ap;
     HIPCHK(hipMemsetAsync(arena, 0, total, c->stream));
@@ -644,7 +676,7 @@ void decoder_step_fused(osw_ctx* c, int nb, int group, bool gather) {
         ProArgs pa{};
         pa.ln = ResLnArgs{embed ? nullptr : ps[last], ks, (int64_t)nb * D, bias, xs[xi], xs[xi ^ 1],
                           WF(c, ln + ".g"), WF(c, ln + ".b"), WH(c, "dec.tok"), WF(c, "dec.pos"), c->cur_tok, c->pos,
-                          ctx, D};
+                          ctx, D, d.n_vocab};
         xi ^= 1;
         return pa;
     };
@@ -729,7 +761,7 @@ void decoder_step(osw_ctx* c, int nb, int group, bool gather) {
     const bool gelu_pro = nb <= GELU_ROWS && !no_gelu_pro && 4 * D / skinny_ksplit(D, 4 * D) <= GELU_KC;
     // x = tok_emb[tok] + pos_emb[pos]; xdn = LN1_0(x)
     launch_dec_resid_ln(nullptr, 0, nb, D, nullptr, c->xd, WF(c, "dec.l0.ln1.g"), WF(c, "dec.l0.ln1.b"), c->xdn, lo_d,
-                        WH(c, "dec.tok"), WF(c, "dec.pos"), c->cur_tok, c->pos, ctx, c->stream);
+                        WH(c, "dec.tok"), WF(c, "dec.pos"), c->cur_tok, c->pos, ctx, d.n_vocab, c->stream);
     for (int l = 0; l < L; ++l) {
         const std::string p = "dec.l" + std::to_string(l);
         int ks = partial(c->xdn, D, WH(c, p + ".qkv.w"), 3 * D, D);
@@ -737,7 +769,7 @@ void decoder_step(osw_ctx* c, int nb, int group, bool gather) {
                              H, ctx, c->dattn, lo_d, gather ? c->anc : nullptr, group, c->sel, c->stream);
         ks = partial(c->dattn, D, WH(c, p + ".o.w"), D, D);
         launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".o.b"), c->xd, WF(c, p + ".ln2.g"), WF(c, p + ".ln2.b"),
-                            c->xdn, lo_d, nullptr, nullptr, nullptr, nullptr, ctx, c->stream);
+                            c->xdn, lo_d, nullptr, nullptr, nullptr, nullptr, ctx, d.n_vocab, c->stream);
         ks = partial(c->xdn, D, WH(c, p + ".xq.w"), D, D);
         {
             Timed t(c, CL_XATTN, 2.0 * nb * H * (double)T_ENC * 64 * 2);
@@ -747,7 +779,7 @@ void decoder_step(osw_ctx* c, int nb, int group, bool gather) {
         }
         ks = partial(c->dattn, D, WH(c, p + ".xo.w"), D, D);
         launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".xo.b"), c->xd, WF(c, p + ".ln3.g"), WF(c, p + ".ln3.b"),
-                            c->xdn, lo_d, nullptr, nullptr, nullptr, nullptr, ctx, c->stream);
+                            c->xdn, lo_d, nullptr, nullptr, nullptr, nullptr, ctx, d.n_vocab, c->stream);
         // (a whole-K fc1 with the GELU epilogue fused has only N/64 = 80 workgroups at
         // turbo: 22.7 us vs 9.6 + 4.7 us for split-K + reduce, measured)
         ks = partial(c->xdn, D, WH(c, p + ".fc1.w"), 4 * D, D);
@@ -766,7 +798,7 @@ void decoder_step(osw_ctx* c, int nb, int group, bool gather) {
         }
         const std::string nx = l + 1 < L ? "dec.l" + std::to_string(l + 1) + ".ln1" : std::string("dec.lnpost");
         launch_dec_resid_ln(fc2_part, ks, nb, D, WF(c, p + ".fc2.b"), c->xd, WF(c, nx + ".g"), WF(c, nx + ".b"), c->xdn,
-                            lo_d, nullptr, nullptr, nullptr, nullptr, ctx, c->stream);
+                            lo_d, nullptr, nullptr, nullptr, nullptr, ctx, d.n_vocab, c->stream);
     }
     GemmArgs gl = gemm_plain(c->xdn, D, WH(c, "dec.tok"), nullptr, nb, d.n_vocab, D, c->logits, d.n_vocab, EPI_F32);
     gl.A_lo = c->xdn + lo_d;
@@ -988,6 +1020,11 @@ void log_mel(osw_ctx* c, const int16_t* pcm, const int64_t* offsets, int n, int 
     }
     if (n > c->clips_cap) {
         const int cap = std::max(n, 2 * c->clips_cap);
+        // superseded buffers are freed (hipFree waits for the device), not kept until destroy
+        dfree(c->offsets, c->owned);
+        dfree(c->mel_off_d, c->owned);
+        dfree(c->nframes_d, c->owned);
+        dfree(c->clip_max, c->owned);
         c->offsets = dalloc<int64_t>(cap + 1, c->owned);
         c->mel_off_d = dalloc<int64_t>(cap + 1, c->owned);
         c->nframes_d = dalloc<int>(cap, c->owned);
@@ -1005,12 +1042,14 @@ void log_mel(osw_ctx* c, const int16_t* pcm, const int64_t* offsets, int n, int 
     }
     if ((size_t)c->mel_off[n] > c->logmel_cap) {
         c->logmel_cap = (size_t)c->mel_off[n] + (size_t)c->mel_off[n] / 2;
+        dfree(c->logmel, c->owned);
         c->logmel = dalloc<float>(c->logmel_cap, c->owned);
     }
     const int16_t* src = pcm + offsets[0];
     if (!on_device) {
         if ((size_t)total > c->pcm_cap) {
             c->pcm_cap = (size_t)total + (size_t)total / 2 + 1;
+            dfree(c->pcm, c->owned);
             c->pcm = dalloc<int16_t>(c->pcm_cap, c->owned);
         }
         if (total) HIPCHK(hipMemcpyAsync(c->pcm, src, (size_t)total * 2, hipMemcpyHostToDevice, c->stream));
@@ -1059,7 +1098,7 @@ IngestDev& ingest_dev(int device) {
         HIPCHK(hipGetDeviceCount(&ndev));
         REQUIRE(device >= 0 && device < ndev, "device ordinal out of range");
         p.reset(new IngestDev());
-        HIPCHK(hipSetDevice(device));
+        DeviceScope dev_scope_((device));
         HIPCHK(hipStreamCreateWithFlags(&p->s, hipStreamNonBlocking));
         p->leaves = dalloc<int2>(128, p->owned);
     }
@@ -1069,8 +1108,11 @@ IngestDev& ingest_dev(int device) {
 template <typename T>
 T* grow(T*& ptr, size_t& cap, size_t n, std::vector<void*>& owned) {
     if (n > cap) {
+        // the caller holds the device mutex and its last call synchronised the stream, so
+        // the old buffer is idle: free it rather than keep every superseded size alive
+        dfree(ptr, owned);
         cap = n + n / 2 + 1024;
-        ptr = dalloc<T>(cap, owned);   // old buffer stays owned until the process exits (rare growth)
+        ptr = dalloc<T>(cap, owned);
     }
     return ptr;
 }
@@ -1186,7 +1228,7 @@ int osw_create(const osw_dims* dims, int32_t device, int32_t max_batch, osw_ctx*
         c->R = max_batch * 5;  // room for the reference's beam_size = 5 at full batch
         c->C1 = (dims->n_mels + 63) / 64 * 64;
         if (const char* e = std::getenv("OSW_NO_GRAPH")) c->use_graph = !(e[0] == '1');
-        HIPCHK(hipSetDevice(device));
+        DeviceScope dev_scope_((device));
         make_streams(c);
         const char* eb = std::getenv("OSW_ENC_BATON");
         if (!eb || eb[0] != '0') {
@@ -1222,7 +1264,7 @@ int osw_create_sibling(osw_ctx* parent, int32_t max_batch, osw_ctx** out) {
         c->R = max_batch * 5;
         c->C1 = parent->C1;
         c->use_graph = parent->use_graph;
-        HIPCHK(hipSetDevice(c->device));
+        DeviceScope dev_scope_((c->device));
         make_streams(c);
         c->w = parent->w;          // same device pointers
         c->arena = parent->arena;  // keeps the weights alive past the parent's destroy
@@ -1247,7 +1289,7 @@ int osw_destroy(osw_ctx* c) {
     return guard([&] {
         {
             std::lock_guard<std::mutex> lk(c->mu);
-            HIPCHK(hipSetDevice(c->device));
+            DeviceScope dev_scope_((c->device));
             HIPCHK(hipStreamSynchronize(c->stream));
             for (auto& e : c->evs) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
             for (auto e : c->ev_free) (void)hipEventDestroy(e);
@@ -1266,7 +1308,7 @@ int osw_set_weight(osw_ctx* c, const char* name, const void* host, int64_t nbyte
         REQUIRE(c && name && host, "null argument");
         std::lock_guard<std::mutex> lk(c->mu);
         REQUIRE(!c->sibling, "sibling contexts share their parent's weights (read-only)");
-        HIPCHK(hipSetDevice(c->device));
+        DeviceScope dev_scope_((c->device));
         Tensor& t = W(c, name);
         const std::string nm(name);
         if (nm == "enc.conv1.w" && c->C1 != c->d.n_mels) {
@@ -1290,7 +1332,7 @@ int osw_get_weight(osw_ctx* c, const char* name, void* host, int64_t nbytes) {
     return guard([&] {
         REQUIRE(c && name && host, "null argument");
         std::lock_guard<std::mutex> lk(c->mu);
-        HIPCHK(hipSetDevice(c->device));
+        DeviceScope dev_scope_((c->device));
         Tensor& t = W(c, name);
         REQUIRE(nbytes == t.numel * (t.f16 ? 2 : 4), std::string("tensor ") + name + ": wrong byte count");
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -1304,7 +1346,7 @@ int osw_init_weight_uniform(osw_ctx* c, const char* name, uint64_t seed, int64_t
         REQUIRE(c && name, "null argument");
         std::lock_guard<std::mutex> lk(c->mu);
         REQUIRE(!c->sibling, "sibling contexts share their parent's weights (read-only)");
-        HIPCHK(hipSetDevice(c->device));
+        DeviceScope dev_scope_((c->device));
         Tensor& t = W(c, name);
         REQUIRE(!(std::string(name) == "enc.conv1.w" && c->C1 != c->d.n_mels),
                 "enc.conv1.w needs osw_set_weight when n_mels is not a multiple of 64");
@@ -1333,7 +1375,7 @@ int osw_log_mel(osw_ctx* c, const int16_t* pcm, const int64_t* offsets, int32_t 
     return guard([&] {
         REQUIRE(c, "null ctx");
         std::lock_guard<std::mutex> lk(c->mu);
-        HIPCHK(hipSetDevice(c->device));
+        DeviceScope dev_scope_((c->device));
         log_mel(c, pcm, offsets, n_clips, pcm_on_device, n_frames);
         HIPCHK(hipStreamSynchronize(c->stream));
         resolve_events(c);
@@ -1344,7 +1386,7 @@ int osw_get_mel(osw_ctx* c, int32_t clip, float* out, int64_t out_floats) {
     return guard([&] {
         REQUIRE(c && out, "null argument");
         std::lock_guard<std::mutex> lk(c->mu);
-        HIPCHK(hipSetDevice(c->device));
+        DeviceScope dev_scope_((c->device));
         REQUIRE(clip >= 0 && clip < c->n_clips, "clip out of range");
         const int nf = c->nframes[clip];
         const int64_t n = (int64_t)nf * c->d.n_mels;
@@ -1363,7 +1405,7 @@ int osw_encode_windows(osw_ctx* c, const osw_window* windows, int32_t n) {
     return guard([&] {
         REQUIRE(c && windows, "null argument");
         std::lock_guard<std::mutex> lk(c->mu);
-        HIPCHK(hipSetDevice(c->device));
+        DeviceScope dev_scope_((c->device));
         encode(c, windows, n);
         HIPCHK(hipStreamSynchronize(c->stream));
         resolve_events(c);
@@ -1374,7 +1416,7 @@ int osw_get_encoder_output(osw_ctx* c, int32_t window, float* out, int64_t out_f
     return guard([&] {
         REQUIRE(c && out, "null argument");
         std::lock_guard<std::mutex> lk(c->mu);
-        HIPCHK(hipSetDevice(c->device));
+        DeviceScope dev_scope_((c->device));
         REQUIRE(window >= 0 && window < c->n_encoded, "window out of range");
         const int64_t n = (int64_t)T_ENC * c->d.n_audio_state;
         REQUIRE(out_floats >= n, "output buffer too small");
@@ -1388,7 +1430,7 @@ int osw_decode_windows(osw_ctx* c, int32_t n, const osw_decode_opts* opts, osw_w
     return guard([&] {
         REQUIRE(c, "null ctx");
         std::lock_guard<std::mutex> lk(c->mu);
-        HIPCHK(hipSetDevice(c->device));
+        DeviceScope dev_scope_((c->device));
         decode(c, n, opts, res);
         resolve_events(c);
     });
@@ -1399,7 +1441,7 @@ int osw_transcribe_batch(osw_ctx* c, const int16_t* pcm, const int64_t* offsets,
     return guard([&] {
         REQUIRE(c, "null ctx");
         std::lock_guard<std::mutex> lk(c->mu);
-        HIPCHK(hipSetDevice(c->device));
+        DeviceScope dev_scope_((c->device));
         REQUIRE(n_clips >= 1 && n_clips <= c->B, "n_clips out of range");
         log_mel(c, pcm, offsets, n_clips, pcm_on_device, nullptr);
         std::vector<osw_window> wins(n_clips);
@@ -1415,7 +1457,7 @@ int osw_encoder_layer_debug(osw_ctx* c, int32_t layer, const float* x, float* y,
     return guard([&] {
         REQUIRE(c && x && y, "null argument");
         std::lock_guard<std::mutex> lk(c->mu);
-        HIPCHK(hipSetDevice(c->device));
+        DeviceScope dev_scope_((c->device));
         REQUIRE(c->finalized, "weights not finalized");
         REQUIRE(T == T_ENC, "T must be 1500");
         REQUIRE(layer >= 0 && layer < c->d.n_audio_layer, "layer out of range");
@@ -1435,7 +1477,7 @@ int osw_debug_gemm(osw_ctx* c, int32_t M, int32_t N, int32_t K, int32_t variant,
         REQUIRE(M >= 1 && N >= 1 && K >= 64 && K % 64 == 0 && iters >= 1, "bad GEMM shape");
         REQUIRE(variant != 3 || (M <= 64 && K % 128 == 0), "skinny needs M <= 64 and K % 128 == 0");
         std::lock_guard<std::mutex> lk(c->mu);
-        HIPCHK(hipSetDevice(c->device));
+        DeviceScope dev_scope_((c->device));
         std::vector<void*> tmp;
         h16* dA = dalloc<h16>((size_t)M * K, tmp);
         h16* dW = dalloc<h16>((size_t)N * K, tmp);
@@ -1502,7 +1544,7 @@ int osw_ingest_mean_square(int32_t device, const int16_t* pcm, int64_t n_frames,
         REQUIRE(n_frames >= 1 && channels >= 1 && channels <= 64, "bad PCM shape");
         IngestDev& g = ingest_dev(device);
         std::lock_guard<std::mutex> lk(g.mu);
-        HIPCHK(hipSetDevice(device));
+        DeviceScope dev_scope_((device));
         const size_t n = (size_t)n_frames * channels;
         grow(g.in, g.in_cap, n, g.owned);
         HIPCHK(hipMemcpyAsync(g.in, pcm, n * 2, hipMemcpyHostToDevice, g.s));
@@ -1517,7 +1559,7 @@ int osw_ingest_apply_gain(int32_t device, const int16_t* pcm, int64_t n_frames, 
         REQUIRE(n_frames >= 1 && channels >= 1 && channels <= 64, "bad PCM shape");
         IngestDev& g = ingest_dev(device);
         std::lock_guard<std::mutex> lk(g.mu);
-        HIPCHK(hipSetDevice(device));
+        DeviceScope dev_scope_((device));
         const size_t n = (size_t)n_frames * channels;
         grow(g.in, g.in_cap, n, g.owned);
         grow(g.out, g.out_cap, (size_t)n_frames, g.owned);
@@ -1552,7 +1594,7 @@ int osw_ingest_resample(int32_t device, const int16_t* pcm, int64_t n_in, int32_
             for (int64_t j = 0; j < hpp; ++j) htf[(size_t)(p * hpp + j)] = full[(size_t)((hpp - 1 - j) * up + p)];
         IngestDev& g = ingest_dev(device);
         std::lock_guard<std::mutex> lk(g.mu);
-        HIPCHK(hipSetDevice(device));
+        DeviceScope dev_scope_((device));
         grow(g.in, g.in_cap, (size_t)n_in, g.owned);
         grow(g.out, g.out_cap, (size_t)n_out, g.owned);
         grow(g.taps, g.taps_cap, (size_t)padlen, g.owned);

@@ -31,6 +31,7 @@ struct ResLnArgs {
     const int* pos;
     int ctx;
     int D;
+    int V;              // rows of tok_emb: an id outside [0, V) is clamped into it
 };
 
 // rows r0 .. r0+nr-1 (nr <= NR); emit(r, c, y) receives every LayerNorm output;
@@ -82,7 +83,7 @@ __device__ __forceinline__ void resln_rows(const ResLnArgs& A, int r0, int nr, b
             a4 += s4;
             a1 += s1;
         } else {
-            const int tk = max(A.tok[r0 + r], 0);  // an invalid id (a NaN row's select) must not fault
+            const int tk = min(max(A.tok[r0 + r], 0), A.V - 1);  // defence in depth: select never emits one
             const h16x4 e4 = *(const h16x4*)(A.tok_emb + (int64_t)tk * D + c4);
             const float* pe = A.pos_emb + (int64_t)pos * D;
             a4 = f32x4{(float)e4[0], (float)e4[1], (float)e4[2], (float)e4[3]} + *(const f32x4*)(pe + c4);

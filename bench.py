@@ -172,7 +172,8 @@ def cpu_baseline(dims, n_tokens_per_clip: float, decode_steps: int) -> dict:
                       f"{t2 - t1:.2f}s + {how}"}
 
 
-def stream_sessions(n_sessions: int, speech_s: float, model: str = "random:large-v3-turbo") -> dict:
+def stream_sessions(n_sessions: int, speech_s: float, model: str = "random:large-v3-turbo", backend=None,
+                    record: list | None = None) -> dict:
     """BASELINE configs[4]: n concurrent streaming sessions against the drop-in backend,
     following src/streaming.py's control flow with a scripted VAD (the reference's own
     test stand-in, tests/test_streaming_session_runtime.py:53-58): 100 ms chunks arrive in
@@ -191,7 +192,8 @@ def stream_sessions(n_sessions: int, speech_s: float, model: str = "random:large
     from open_speech_amd.backend import HipWhisperBackend
 
     os.environ.setdefault("STT_HIP_TOKENS_PER_SEC", "4")
-    be = HipWhisperBackend()
+    own = backend is None
+    be = HipWhisperBackend() if own else backend
     be.load_model(model)
     ex = ThreadPoolExecutor(max_workers=4, thread_name_prefix="stream-transcribe")
     chunk = 1600
@@ -208,9 +210,11 @@ def stream_sessions(n_sessions: int, speech_s: float, model: str = "random:large
                 return
             wav = pcm_to_wav(bytes(utter), 16000)
             ts = time.perf_counter()
-            await loop.run_in_executor(ex, lambda: be.transcribe(audio=wav, model=model, language=None,
-                                                                 response_format="json", temperature=0.0))
+            r = await loop.run_in_executor(ex, lambda: be.transcribe(audio=wav, model=model, language=None,
+                                                                     response_format="json", temperature=0.0))
             lat.append(time.perf_counter() - ts)
+            if record is not None:
+                record.append((i, wav, r))
 
         n = len(pcm) // (2 * chunk)
         for c in range(n):
@@ -240,7 +244,8 @@ def stream_sessions(n_sessions: int, speech_s: float, model: str = "random:large
     asyncio.run(main())
     wall = time.perf_counter() - wall0
     ex.shutdown(wait=True)
-    be.unload_model(model)
+    if own:
+        be.unload_model(model)
     audio = n_sessions * (speech_s + silence_s)
     return {"sessions": n_sessions, "speech_s_per_session": speech_s, "chunk_ms": 100, "executor_threads": 4,
             "transcriptions": len(lat), "transcriptions_per_s": round(len(lat) / wall, 1),
@@ -251,6 +256,53 @@ def stream_sessions(n_sessions: int, speech_s: float, model: str = "random:large
             "audio_seconds": audio, "wall_s": round(wall, 2),
             "realtime_factor": round(audio / wall, 2),
             "note": "scripted VAD (speech then 0.5 s silence), 4 tokens/s length control, beam 5, random weights"}
+
+
+def ingest_timing(repeats: int = 30, device: int = 0) -> dict:
+    """The GPU ingest drop-ins (open_speech_amd/ingest.py) against the host numpy / scipy
+    operations the reference runs for the same calls (src/audio/preprocessing.py:53-63
+    for a 30 s upload, src/streaming.py:55-91 for one 100 ms 48 kHz client chunk), both
+    timed here with bytes in and bytes out (median of `repeats` after 3 warm-ups).  The
+    host side is written out inline for timing only."""
+    import io
+    import wave
+
+    from scipy.signal import resample_poly
+
+    from open_speech_amd import ingest
+
+    wav30 = synth.to_wav_bytes(synth.chirp_clip(7, 30.0))
+    t = np.arange(4800) / 48000.0
+    chunk = (np.sin(2 * np.pi * 1000.0 * t) * 0.5 * 32767).astype(np.int16).tobytes()
+
+    def host_pre(wav):
+        with wave.open(io.BytesIO(wav), "rb") as wf:
+            sr, raw = wf.getframerate(), wf.readframes(wf.getnframes())
+        a = np.frombuffer(raw, np.int16).astype(np.float32) / 32768.0
+        rms = np.sqrt(np.mean(np.square(a)))
+        if rms > 1e-8:
+            a = np.clip(a * 10 ** ((-18.0 - 20 * np.log10(rms)) / 20), -1.0, 1.0)
+        return synth.to_wav_bytes((np.clip(a, -1.0, 1.0) * 32767.0).astype(np.int16), sr)
+
+    def host_rs(pcm):
+        x = np.frombuffer(pcm, np.int16).astype(np.float32)
+        return np.clip(resample_poly(x, 1, 3), -32768, 32767).astype(np.int16).tobytes()
+
+    def med(f, arg):
+        for _ in range(3):
+            f(arg)
+        ts = []
+        for _ in range(repeats):
+            t0 = time.perf_counter()
+            f(arg)
+            ts.append((time.perf_counter() - t0) * 1e3)
+        return round(float(np.median(ts)), 3)
+
+    gpu_pre = lambda w: ingest.preprocess_stt_audio(w, noise_reduce=False, normalize=True, device=device)  # noqa
+    gpu_rs = lambda p: ingest.resample_pcm16(p, 48000, 16000, device=device)  # noqa: E731
+    return {"preprocess_30s_wav": {"gpu_ms": med(gpu_pre, wav30), "host_numpy_ms": med(host_pre, wav30)},
+            "resample_100ms_48k_chunk": {"gpu_ms": med(gpu_rs, chunk), "host_scipy_ms": med(host_rs, chunk)},
+            "repeats": repeats, "note": "bytes in, bytes out; host = the reference's numpy/scipy ops, one thread"}
 
 
 def timed_steps(dp, allpcm, k: int, dist=None, dev=None):
@@ -466,6 +518,10 @@ def main(argv=None):
         if a.stream_sessions > 0 and world == 1:
             stream = stream_sessions(a.stream_sessions, a.stream_speech_s)
 
+        ingest_t = None
+        if world == 1:
+            ingest_t = ingest_timing(device=dev.index)
+
         cpu = None
         if not a.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(dims, tokens_per_clip, a.cpu_decode_steps)
@@ -485,6 +541,7 @@ def main(argv=None):
             "beam5": beam5_lanes,
             "realistic_lengths": realistic,
             "streaming": stream,
+            "ingest": ingest_t,
             "beam5_audio_sec_per_sec_1lane": beam5,
             "realtime_factor": round(value, 1),
             "roofline": roof,

@@ -97,12 +97,31 @@ def preprocess_stt_audio(wav_bytes: bytes, *, noise_reduce: bool, normalize: boo
         # the reference returns non-WAV / non-16-bit input unchanged (preprocessing.py:54-58)
         return wav_bytes
     if noise_reduce:
-        try:
-            import noisereduce  # noqa: F401  # type: ignore
-        except ImportError as e:
-            raise RuntimeError("Noise reduction requires optional dependency: pip install 'open-speech[noise]'") from e
-        raise RuntimeError("noise reduction is not offloaded to the GPU; call the reference's preprocess_stt_audio")
+        return _write_wav(_denoised_pcm16(pcm, sr, channels, normalize), sr)
     return _write_wav(normalize_pcm16(pcm, channels, normalize, device), sr)
+
+
+def _denoised_pcm16(pcm: np.ndarray, sr: int, channels: int, normalize: bool) -> np.ndarray:
+    """STT_NOISE_REDUCE (src/config.py:166): the reference's chain on the host,
+    preprocessing.py:59-63 — float32 mono, noisereduce's spectral gating (a host
+    library, as in the reference), normalize_gain, clip, x 32767, truncating cast.
+    The gain is applied to the denoised float signal, so it stays in numpy here (the
+    GPU gain kernel takes int16 input); the same RuntimeError as the reference when the
+    optional dependency is absent."""
+    try:
+        import noisereduce as nr  # type: ignore
+    except ImportError as e:
+        raise RuntimeError("Noise reduction requires optional dependency: pip install 'open-speech[noise]'") from e
+    audio = pcm.astype(np.float32) / 32768.0
+    if channels > 1:
+        audio = audio.reshape(-1, channels).mean(axis=1)
+    audio = nr.reduce_noise(y=audio, sr=sr)
+    if normalize:
+        rms = np.sqrt(np.mean(np.square(audio)))
+        if rms > 1e-8:
+            gain = 10 ** ((-18.0 - 20 * np.log10(rms)) / 20)
+            audio = np.clip(audio * gain, -1.0, 1.0)
+    return (np.clip(audio, -1.0, 1.0) * 32767.0).astype(np.int16)
 
 
 @lru_cache(maxsize=32)

@@ -52,6 +52,23 @@ def preprocess_cases():
     yield "empty_data", to_wav_bytes(np.zeros(0, np.int16))
 
 
+def noise_cases():
+    """(name, wav bytes) for preprocess_stt_audio(noise_reduce=True)."""
+    yield "chirp30", to_wav_bytes(chirp_clip(0, 30.0))
+    st = np.stack([_scaled(3, 2.0, 0.5), _scaled(4, 2.0, 0.3)], axis=1)
+    yield "stereo2", _wav(st, 16000, ch=2)
+    yield "silence2", to_wav_bytes(np.zeros(32000, np.int16))
+
+
+def standin_reduce_noise(y: np.ndarray, sr: int) -> np.ndarray:
+    """A deterministic stand-in for ``noisereduce.reduce_noise`` (the optional
+    dependency is absent on both machines): halves the signal and adds a fixed
+    low-level tone, so the chain around it (float32 mono in, gain + clip + truncating
+    cast out) is what the fixture pins."""
+    t = np.arange(y.size, dtype=np.float32)
+    return (y * np.float32(0.5) + np.float32(0.01) * np.sin(t * np.float32(0.01))).astype(np.float32)
+
+
 def resample_cases():
     """(name, pcm16 bytes, from_rate, to_rate) for resample_pcm16."""
     for sr, secs in ((8000, 2.0), (22050, 1.5), (44100, 2.0), (48000, 3.0), (11025, 0.7), (32000, 1.0)):

@@ -52,6 +52,9 @@ class TranscribeOptions:
     best_of: int = 5               # faster-whisper default; used when temperature > 0
     prompt_reset_on_temperature: float = 0.5
     seed: int = 0
+    # faster-whisper's max_new_tokens: a window's decode stops after this many sampled
+    # tokens (max_length = prompt length + max_new_tokens, which may not exceed 448)
+    max_new_tokens: int | None = None
     # bench-only length control (STT_HIP_TOKENS_PER_SEC): random weights never emit
     # <|endoftext|>, so each window's decode is cut at ceil(rate * window seconds) + 2
     tokens_per_second: float | None = None
@@ -59,7 +62,8 @@ class TranscribeOptions:
     def key(self):
         return (self.task, self.language, self.initial_prompt, self.condition_on_previous_text,
                 self.without_timestamps, tuple(self.suppress_tokens), self.suppress_blank, self.beam_size,
-                self.patience, self.length_penalty, self.temperature, self.best_of, self.tokens_per_second)
+                self.patience, self.length_penalty, self.temperature, self.best_of, self.tokens_per_second,
+                self.max_new_tokens)
 
 
 @dataclass
@@ -166,7 +170,14 @@ def transcribe_clips(engine, pcm_list: list, opts: TranscribeOptions, tok: Whisp
                     wins.append((s.idx, s.seek, size))
                 engine.encode(wins)
                 langs = None if _detect else [s.lang_token for s, _ in chunk]
-                cfg = DecodeConfig(task=opts.task, language_token=None, suppress_tokens=suppress,
+                max_length = 448
+                if opts.max_new_tokens is not None:
+                    max_length = _plen + 3 + (1 if opts.without_timestamps else 0) + int(opts.max_new_tokens)
+                    if max_length > 448:
+                        raise ValueError(f"the prompt is {max_length - int(opts.max_new_tokens)} tokens and "
+                                         f"max_new_tokens is {opts.max_new_tokens}: their sum exceeds the "
+                                         "model's maximum length (448)")
+                cfg = DecodeConfig(max_length=max_length, task=opts.task, language_token=None, suppress_tokens=suppress,
                                    suppress_blank=opts.suppress_blank, without_timestamps=opts.without_timestamps,
                                    max_initial_timestamp_index=max_init, beam_size=beam, patience=opts.patience,
                                    length_penalty=opts.length_penalty, temperature=opts.temperature,

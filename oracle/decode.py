@@ -34,6 +34,11 @@ def logsumexp(x: np.ndarray) -> float:
     return float(m + np.log(np.sum(np.exp(x - m))))
 
 
+# the model's maximum decoder length: previous text keeps its last 448 // 2 - 1 tokens
+# whatever max_length a call uses (faster-whisper get_prompt uses self.max_length = 448)
+MODEL_MAX_LENGTH = 448
+
+
 @dataclass
 class DecodeOptions:
     suppress_blank: bool = True
@@ -110,7 +115,7 @@ def greedy_from_encoder(oracle, xkv, st, *, language=None, task=None, prev_token
     prompt = []
     if prev_tokens:
         prompt.append(st.sot_prev)
-        prompt.extend(list(prev_tokens)[-(opts.max_length // 2 - 1):])
+        prompt.extend(list(prev_tokens)[-(MODEL_MAX_LENGTH // 2 - 1):])
     sot_index = len(prompt)
     prompt.append(st.sot)
     pos = 0
@@ -190,7 +195,7 @@ def beam_from_encoder(oracle, xkv, st, *, language=None, task=None, prev_tokens=
     prompt = []
     if prev_tokens:
         prompt.append(st.sot_prev)
-        prompt.extend(list(prev_tokens)[-(opts.max_length // 2 - 1):])
+        prompt.extend(list(prev_tokens)[-(MODEL_MAX_LENGTH // 2 - 1):])
     prompt.append(st.sot)
     pos = 0
     for t in prompt:

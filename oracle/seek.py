@@ -77,11 +77,14 @@ def split_by_timestamps(tokens, tb, time_offset, segment_size, segment_duration,
     return segs, seek
 
 
-def seek_loop(decode_window, n_frames: int, st, decode_text, opts: SeekOptions = SeekOptions()):
+def seek_loop(decode_window, n_frames: int, st, decode_text, opts: SeekOptions = SeekOptions(),
+              initial_tokens=()):
     """decode_window(seek, size, prev_tokens) -> (tokens, sum_logprob, no_speech_prob);
-    decode_text(tokens) -> str.  Returns the list of Windows in order."""
+    decode_text(tokens) -> str; initial_tokens: the encoded initial prompt
+    (``tokenizer.encode(" " + initial_prompt.strip())``), the first previous text.
+    Returns the list of Windows in order."""
     content = max(0, n_frames - 1)
-    seek, all_tokens, reset_since, out = 0, [], 0, []
+    seek, all_tokens, reset_since, out = 0, list(initial_tokens), 0, []
     while seek < content:
         size = min(N_FRAMES, content - seek)
         prev = all_tokens[reset_since:]

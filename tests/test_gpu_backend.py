@@ -55,17 +55,26 @@ def test_silence_and_short_clips(backend):
         assert "segments" in r
 
 
-def test_backend_verbose_json_matches_oracle_seek_loop(monkeypatch):
+@pytest.mark.parametrize("variant", ["greedy", "tokenizer_prompt"])
+def test_backend_verbose_json_matches_oracle_seek_loop(monkeypatch, tmp_path, variant):
     """SURVEY §8a rows a1/a5 through the boundary: HipWhisperBackend.transcribe (WAV bytes
     in, the reference's verbose_json out, src/backends/faster_whisper.py:249-270) on a 75 s
     clip, greedy, with every window the backend's runner encoded and decoded checked
     against the oracle's generate_segments restatement (oracle/seek.py) decoding the GPU's
-    own encoder output, and the returned segments equal to the oracle's."""
+    own encoder output, and the returned segments equal to the oracle's.
+    "tokenizer_prompt": the model is a transformers-layout directory (config.json,
+    model.safetensors, tokenizer.json: tests/tokfix.py) at micro dims, the request carries
+    a prompt (faster-whisper initial_prompt): the first window's prompt is
+    [<|startofprev|>] + encode(" " + prompt), the non-speech set comes from the
+    tokenizer, and every segment's text / compression_ratio are the tokenizer's."""
+    import zlib
+
+    import tokfix
     from oracle import decode as odec
     from oracle import seek as oseek
     from oracle.model import WhisperOracle
     from open_speech_amd import dims as D
-    from open_speech_amd import weights
+    from open_speech_amd import model_store, weights
     from open_speech_amd.engine import WhisperEngine
     from open_speech_amd.tokenizer import WhisperTokenizer, get_suppressed_tokens
 
@@ -95,43 +104,62 @@ def test_backend_verbose_json_matches_oracle_seek_loop(monkeypatch):
         recs.append(r)
         return r
 
+    if variant == "greedy":
+        mid, prompt = MID, None
+    else:
+        mid, prompt = tokfix.make_hf_model_dir(str(tmp_path / "micro_hf"), D.MICRO_TEST), "  Budget review, part two. "
     monkeypatch.setenv("STT_HIP_BEAM_SIZE", "1")
     monkeypatch.setenv("STT_HIP_MAX_BATCH", "2")
     monkeypatch.setenv("STT_HIP_GPUS", "0")
     monkeypatch.setenv("STT_HIP_LANES", "1")  # one lane: every window goes through the recorder
     b = HipWhisperBackend(engine_factory=factory)
-    b.load_model(MID)
+    b.load_model(mid)
     try:
         pcm = synth.chirp_clip(41, 75.0)
-        r = b.transcribe(synth.to_wav_bytes(pcm), MID, response_format="verbose_json")
+        r = b.transcribe(synth.to_wav_bytes(pcm), mid, response_format="verbose_json", prompt=prompt)
     finally:
-        b.unload_model(MID)
+        b.unload_model(mid)
     assert len(recs) == 1
     rec = recs[0]
     assert len(rec.calls) >= 3, "a 75 s clip needs at least three 30 s windows"
-    d = D.TINY_TEST
-    w = weights.random_weights(d, seed=1234)  # the values init_random(seed=1234) writes on the device
-    tok = WhisperTokenizer(d.n_vocab)
+    if variant == "greedy":
+        d = D.TINY_TEST
+        w = weights.random_weights(d, seed=1234)  # the values init_random(seed=1234) writes on the device
+        tok = WhisperTokenizer(d.n_vocab)
+    else:
+        src = model_store.resolve(mid)
+        d, w = src.dims, model_store.load_weights(src)
+        tok = WhisperTokenizer(d.n_vocab, src.tokenizer_json)
+        assert tok.has_text
     st = tok.special
     sup = get_suppressed_tokens(tok, [-1])
+    init = tok.encode(" " + prompt.strip()) if prompt else []
     orc = WhisperOracle(d, w, fp16=True)
     gpu = {(s, z): (p, o) for s, z, p, o in rec.calls}
     lang = {}
 
-    def decode_window(seek, size, prompt):
+    def decode_window(seek, size, prompt_toks):
         enc = rec.enc[(seek, size)]
         o = odec.greedy_from_encoder(orc, orc.cross_kv(enc), st, language=lang.get("tok"),
-                                     prev_tokens=prompt[1:], opts=odec.DecodeOptions(suppress_tokens=sup))
+                                     prev_tokens=prompt_toks[1:], opts=odec.DecodeOptions(suppress_tokens=sup))
         lang.setdefault("tok", o.language)
         gp, go = gpu[(seek, size)]
-        assert gp == prompt, f"window {seek}: prompt differs"
+        assert gp == prompt_toks, f"window {seek}: prompt differs"
         assert go.tokens == o.tokens, f"window {seek}: ids differ from the oracle's"
         return go.tokens, go.sum_logprob, go.no_speech_prob
 
     nf = (len(pcm) + 160) // 160
-    wins = oseek.seek_loop(decode_window, nf, st, tok.decode)
+    wins = oseek.seek_loop(decode_window, nf, st, tok.decode, initial_tokens=init)
+    if prompt:
+        assert wins[0].prompt == [st.sot_prev] + init
     want = [(a, b_, t) for x in wins for a, b_, t in x.segments]
     got = [(s["start"], s["end"], s["tokens"]) for s in r["segments"]]
     assert [(round(a, 6), round(e, 6), t) for a, e, t in got] == [(round(a, 6), round(e, 6), t) for a, e, t in want]
     assert r["task"] == "transcribe" and r["duration"] == pytest.approx(75.0)
     assert [s["id"] for s in r["segments"]] == list(range(len(r["segments"])))
+    # text fields: the tokenizer's decode of each segment, the window text's compression ratio
+    for s in r["segments"]:
+        assert s["text"] == tok.decode(s["tokens"])
+        wt = tok.decode(gpu[(s["seek"], next(z for sk, z in gpu if sk == s["seek"]))][1].tokens).strip().encode()
+        assert s["compression_ratio"] == (len(wt) / len(zlib.compress(wt)) if wt else 0.0)
+    assert r["text"] == "".join(s["text"] for s in r["segments"]).strip()

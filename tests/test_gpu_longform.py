@@ -83,3 +83,51 @@ def test_longform_seek_loop_matches_oracle():
         assert res.duration == pytest.approx(75.0)
     finally:
         eng.close()
+
+
+def test_longform_beam5_seek_loop_matches_oracle():
+    """The reference's decoding (beam_size 5, src/backends/faster_whisper.py:237) inside
+    the seek loop: a 75 s clip through transcribe_clips with beam 5, every window's
+    prompt and ids equal to the oracle's CTranslate2-BeamSearch restatement decoding the
+    GPU's own encoder output, and the same segments.  faster-whisper's max_new_tokens
+    (24 per window) bounds the oracle's cost: random weights never emit <|endoftext|>."""
+    from oracle import decode as odec
+    from oracle import seek as oseek
+    from oracle.model import WhisperOracle
+    d = D.TINY_TEST
+    w = weights.random_weights(d, seed=1234, emb_std=0.5)
+    eng = WhisperEngine(d, device=0, max_batch=2)
+    try:
+        eng.load_weights(w)
+        tok = WhisperTokenizer(d.n_vocab)
+        st = tok.special
+        sup = get_suppressed_tokens(tok, [-1])
+        pcm = synth.chirp_clip(42, 75.0)
+        rec = Recorder(eng)
+        opts = TranscribeOptions(beam_size=5, max_new_tokens=24)
+        res = transcribe_clips(rec, [pcm], opts, tok, sup)[0]
+        gpu = {(s, z): (p, o) for s, z, p, o in rec.calls}
+        assert len(rec.calls) >= 3
+        orc = WhisperOracle(d, w, fp16=True)
+        lang = {}
+
+        def decode_window(seek, size, prompt):
+            enc = rec.enc[(seek, size)]
+            plen = len(prompt) + 3
+            r = odec.beam_from_encoder(orc, orc.cross_kv(enc), st, language=lang.get("tok"), prev_tokens=prompt[1:],
+                                       opts=odec.DecodeOptions(suppress_tokens=sup, max_length=plen + 24),
+                                       beam=odec.BeamOptions(beam_size=5))
+            lang.setdefault("tok", r.language)
+            gp, go = gpu[(seek, size)]
+            assert gp == prompt, f"window {seek}: prompt differs"
+            assert go.tokens == r.tokens, f"window {seek}: GPU beam ids differ from the oracle's"
+            assert abs(go.sum_logprob - r.sum_logprob) <= 1e-4 * (len(r.tokens) + 1) + 1e-3 * abs(r.sum_logprob)
+            return go.tokens, go.sum_logprob, go.no_speech_prob
+
+        nf = (len(pcm) + 160) // 160
+        wins = oseek.seek_loop(decode_window, nf, st, tok.decode)
+        assert [(x.seek, x.size) for x in wins] == [(s, z) for s, z, _, _ in rec.calls]
+        want = [(a, b, t) for x in wins for a, b, t in x.segments]
+        assert [(sg.start, sg.end, sg.tokens) for sg in res.segments] == want
+    finally:
+        eng.close()

@@ -69,3 +69,34 @@ def test_pcm_to_wav_header_matches_reference():
         pcm = b"\x01\x02" * (rec["n_bytes"] // 2)
         h = audio.pcm_to_wav(pcm, rec["rate"])
         assert h[:44].hex() == rec["header_hex"] and sha(h) == rec["sha256"]
+
+
+NOISE = {r["name"]: r for r in META["preprocess_noise"]}
+
+
+@pytest.mark.parametrize("name,wav", list(ref_inputs.noise_cases()), ids=lambda v: v if isinstance(v, str) else "")
+def test_noise_reduce_path_matches_reference(name, wav, monkeypatch):
+    """STT_NOISE_REDUCE=true (src/config.py:166): the drop-in's preprocess_stt_audio runs
+    noisereduce on the host and the reference's float chain after it; with the same
+    stand-in denoiser the bytes equal the reference's own output."""
+    import sys
+    import types
+
+    from open_speech_amd import ingest
+    nr = types.ModuleType("noisereduce")
+    nr.reduce_noise = lambda y, sr: ref_inputs.standin_reduce_noise(y, sr)
+    monkeypatch.setitem(sys.modules, "noisereduce", nr)
+    rec = NOISE[name]
+    assert sha(wav) == rec["in_sha256"], "input generator changed"
+    out = ingest.preprocess_stt_audio(wav, noise_reduce=True, normalize=True)
+    assert len(out) == rec["out_len"] and sha(out) == rec["out_sha256"], name
+
+
+def test_noise_reduce_without_dependency_raises_like_reference(monkeypatch):
+    import sys
+
+    from open_speech_amd import ingest
+    monkeypatch.setitem(sys.modules, "noisereduce", None)    # import fails, as on both machines
+    wav = next(iter(ref_inputs.noise_cases()))[1]
+    with pytest.raises(RuntimeError, match=r"pip install 'open-speech\[noise\]'"):
+        ingest.preprocess_stt_audio(wav, noise_reduce=True, normalize=True)

@@ -191,6 +191,7 @@ def gen_turbo_layer(out):
 TURBO_SEED = 0          # the bench's init_random(seed=0) weights
 TURBO_CLIP = 0          # synth.chirp_clip(0, 30 s)
 TURBO_FULL_STEPS = 4    # full-vocabulary fp32 logits stored for the first steps
+TURBO_FULL_STRIDE = 32  # ... and for every 32nd step after them
 TURBO_SUBSET = 256      # per step: logits of the top-32 tokens and of a fixed token sample
 
 
@@ -235,11 +236,14 @@ def gen_turbo(out):
     sample = np.sort(np.random.default_rng(2024).choice(d.n_vocab, TURBO_SUBSET, replace=False)).astype(np.int32)
     seq = list(prompt)
     ids, lps, top5i, top5v, full, lse, sub_i, sub_v, margins = [], [], [], [], [], [], [], [], []
+    full_steps = []
     sum_lp = 0.0
     while True:
         raw = lg.float().numpy()
-        if len(full) < TURBO_FULL_STEPS:
+        step_i = len(lse)
+        if step_i < TURBO_FULL_STEPS or step_i % TURBO_FULL_STRIDE == 0:
             full.append(raw.copy())
+            full_steps.append(step_i)
         lse.append(float(torch.logsumexp(lg, -1)))
         t32 = np.argsort(-raw, kind="stable")[:32].astype(np.int32)
         sub_i.append(np.concatenate([t32, sample]))
@@ -267,13 +271,65 @@ def gen_turbo(out):
     rows = np.r_[0:8, 700:708, 1492:1500]
     np.savez_compressed(os.path.join(out, "turbo_model.npz"), enc_rows=rows, enc=e[rows].astype(np.float32),
                         enc_rownorm=np.linalg.norm(e.astype(np.float64), axis=1), sot_logits=sot_logits,
-                        full_logits=np.stack(full), lse=np.array(lse), sub_ids=np.stack(sub_i), sub_vals=np.stack(sub_v),
+                        full_logits=np.stack(full), full_steps=np.array(full_steps, np.int32), lse=np.array(lse), sub_ids=np.stack(sub_i), sub_vals=np.stack(sub_v),
                         ids=np.array(ids, np.int32), logprobs=np.array(lps), top5_ids=np.stack(top5i).astype(np.int32),
                         top5_vals=np.stack(top5v), margins=np.array(margins), language=np.int32(lang),
                         no_speech_prob=np.float64(nsp), sum_logprob=np.float64(sum_lp))
     print("turbo: lang", lang, "n_ids", len(ids), "first", ids[:12], "min margin", min(margins))
     return {"seed": TURBO_SEED, "clip": TURBO_CLIP, "language": lang, "n_ids": len(ids),
             "min_top2_margin": min(margins)}
+
+
+TURBO_BEAM_MAX_LEN = 96   # prompt (3) + 93 sampled positions: random weights never emit <|endoftext|>
+
+
+class _HFStepper:
+    """The decoder-step interface of oracle.model.WhisperOracle (new_cache /
+    decoder_step) over the fp32 transformers model, so oracle.decode.beam_from_encoder
+    (the CTranslate2 BeamSearch restatement) runs on transformers' arithmetic."""
+
+    def __init__(self, model, enc):
+        self.model, self.enc = model, enc
+
+    def new_cache(self):
+        return {"past": None}
+
+    def decoder_step(self, tok, pos, cache, xkv):
+        with torch.no_grad():
+            o = self.model(encoder_outputs=(self.enc,), decoder_input_ids=torch.tensor([[int(tok)]]),
+                           past_key_values=cache["past"], use_cache=True)
+        cache["past"] = o.past_key_values
+        return o.logits[0, -1].float().numpy()
+
+
+def gen_turbo_beam(out):
+    """whisper-large-v3-turbo beam search width 5 (the reference's decoding,
+    src/backends/faster_whisper.py:237) in fp32: the oracle's CTranslate2-BeamSearch
+    restatement (oracle/decode.py beam_from_encoder, patience 1, length penalty 1,
+    one hypothesis) driven by the transformers decoder on the same hash-initialised
+    weights and clip as gen_turbo, to TURBO_BEAM_MAX_LEN positions.  Stores the best
+    hypothesis' ids and raw cumulative log-prob, the language and no-speech prob."""
+    from oracle import decode as odec
+
+    d = D.LARGE_V3_TURBO
+    st = D.SpecialTokens.for_vocab(d.n_vocab)
+    w = weights.random_weights(d, seed=TURBO_SEED)
+    model = build_model(d, w)
+    del w
+    pcm = synth.chirp_clip(TURBO_CLIP, 30.0)
+    mel = fe_mel(pcm, d.n_mels)[:, :3000]
+    with torch.no_grad():
+        enc = model.model.encoder(input_features=torch.from_numpy(mel)[None]).last_hidden_state
+    sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+    r = odec.beam_from_encoder(_HFStepper(model, enc), None, st,
+                               opts=odec.DecodeOptions(suppress_tokens=sup, max_length=TURBO_BEAM_MAX_LEN),
+                               beam=odec.BeamOptions(beam_size=5))
+    np.savez_compressed(os.path.join(out, "turbo_beam5.npz"), ids=np.array(r.tokens, np.int32),
+                        sum_logprob=np.float64(r.sum_logprob), language=np.int32(r.language),
+                        no_speech_prob=np.float64(r.no_speech_prob), max_length=np.int32(TURBO_BEAM_MAX_LEN))
+    print("turbo beam5: lang", r.language, "n_ids", len(r.tokens), "sum_lp", r.sum_logprob, "first", r.tokens[:12])
+    return {"seed": TURBO_SEED, "clip": TURBO_CLIP, "beam_size": 5, "max_length": TURBO_BEAM_MAX_LEN,
+            "n_ids": len(r.tokens), "language": int(r.language)}
 
 
 def gen_logits_rules(out):
@@ -323,7 +379,7 @@ def gen_logits_rules(out):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "tests", "golden"))
-    ap.add_argument("--only", default=None, help="comma list of: mel,rules,tiny,turbo_layer,turbo")
+    ap.add_argument("--only", default=None, help="comma list of: mel,rules,tiny,turbo_layer,turbo,turbo_beam")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     torch.manual_seed(0)
@@ -331,7 +387,7 @@ def main():
     meta = json.load(open(mp)) if os.path.exists(mp) else {}
     meta.update({"generator": "tools/make_golden.py", "transformers": __import__("transformers").__version__,
                  "torch": torch.__version__})
-    only = set(a.only.split(",")) if a.only else {"mel", "rules", "tiny", "turbo_layer", "turbo"}
+    only = set(a.only.split(",")) if a.only else {"mel", "rules", "tiny", "turbo_layer", "turbo", "turbo_beam"}
     if "mel" in only:
         meta["mel"] = gen_mel(a.out)
     if "rules" in only:
@@ -342,6 +398,8 @@ def main():
         meta["turbo_layer"] = gen_turbo_layer(a.out)
     if "turbo" in only:
         meta["turbo"] = gen_turbo(a.out)
+    if "turbo_beam" in only:
+        meta["turbo_beam"] = gen_turbo_beam(a.out)
     with open(os.path.join(a.out, "meta.json"), "w") as fh:
         json.dump(meta, fh, indent=1)
 

@@ -121,6 +121,13 @@ struct GemmArgs {
     // nullptr: A alone (fp16 activations).  Supported by the skinny and wide kernels (the
     // decoder's); launch_gemm routes every A_lo GEMM to them.
     const h16* A_lo;
+    // skinny kernel, hi/lo rows in 32-row groups: issue every k32 step of the workgroup's
+    // weights up front (kc <= 256) instead of one chunk ahead (set by the launcher)
+    int preload_w;
+    // skinny kernel, several row groups: a 1-D grid where the row groups of one (column
+    // block, K range) are consecutive workgroups of one XCD (ids 8j + x, j = row group
+    // fastest), so the second group's weight reads hit the L2 the first one filled
+    int pair_rows;
 };
 
 // fp32 -> (hi, lo) fp16 pair: hi = fp16(v), lo = fp16(v - hi)
@@ -142,7 +149,8 @@ int tiled_ksplit(int M, int N, int K);
 void launch_gemm_tiled_partial(const GemmArgs& g, float* part, int ks, hipStream_t s);
 int launch_gemm_skinny_partial(const GemmArgs& g, float* part, hipStream_t s);
 struct ProArgs;
-int launch_gemm_skinny_pro(const GemmArgs& g, int pro, const ProArgs& pa, bool direct, float* part, hipStream_t s);
+int launch_gemm_skinny_pro(const GemmArgs& g, int pro, const ProArgs& pa, bool direct, float* part, hipStream_t s,
+                           bool select = false);
 void launch_layernorm(const float* x, int64_t M, int D, const float* g, const float* b, h16* y, hipStream_t s);
 
 }  // namespace osw

@@ -35,6 +35,24 @@ struct BeamWin {
     float best_norm, best_raw;
 };
 
+// Batch-1 greedy steps: the logits GEMM runs the token selection in its epilogue
+// (gemm.hip, gemm_skinny_kernel<.., SEL>): every workgroup reduces its 64 columns to one
+// slice record, the last to arrive merges them in workgroup order, finalises the row
+// (select.h select_finalize) and advances the step counter -- no select launch.
+struct SelFuse {
+    SelParams P;
+    const float* logits;  // this GEMM's output row (read back by the finaliser)
+    int* pos;
+    const unsigned* supmask;
+    const int* prompt;
+    SelState* st;
+    int* cur_tok;
+    int* tokens;
+    int max_tokens;
+    void* parts;   // one slice record per logits workgroup
+    int* ticket;   // arrival counter (zero between launches)
+};
+
 constexpr int MAX_BEAM = 8;
 constexpr int XPART = 72;     // floats per (decoder row, head, key chunk) cross-attention partial: m, l, pad, acc[64]
 constexpr int XCHUNKS = 8;    // fixed key chunks per (window, head) in cross-attention
@@ -48,6 +66,7 @@ void launch_beam(const float* logits, int windows, int* pos, const SelParams& P,
                  SelState* st, const void* sel_parts, void* cand, int* seq, int* anc, int ctx, BeamWin* bw,
                  int* best_tok, int* cur_tok, int max_tokens, int* arrive, hipStream_t s);
 int sel_parts_bytes();
+int sel_fused_parts_bytes(int V);  // SelFuse::parts of the batch-1 logits GEMM (one record per 64 columns)
 int beam_cand_bytes(int beam);
 void launch_count_done(const SelState* st, int rows, int* out, hipStream_t s);
 

@@ -23,6 +23,8 @@
 namespace osw {
 
 namespace {
+#include "select.h"
+
 constexpr int BM = 128, BN = 128, BK = 64, NTHR = 256;
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
@@ -426,9 +428,8 @@ void launch256(const GemmArgs& g0, hipStream_t s) {
 // drained inside the loop (raw s_barrier, no __syncthreads).
 constexpr int HT = 128 * BK;  // halfs per half-tile
 
-template <int EPI, bool NOEPI>
-__device__ __forceinline__ void gemm8p_tile(const GemmArgs& g, int bid, h16* smem, int tid) {
-    const int wave = tid >> 6, lane = tid & 63;
+// tile origin of virtual workgroup id `bid` (XCD-contiguous runs, column bands of G tiles)
+__device__ __forceinline__ void tile8p_origin(const GemmArgs& g, int bid, int& m0, int& n0) {
     const int ntn = (g.N + GB - 1) / GB, ntm = (g.M + GB - 1) / GB;
     const int nwg = ntn * ntm;
     const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
@@ -436,20 +437,127 @@ __device__ __forceinline__ void gemm8p_tile(const GemmArgs& g, int bid, h16* sme
     const int G = g.band > 0 ? min(g.band, ntn) : ntn;
     const int band = tile / (G * ntm), rr0 = tile % (G * ntm);
     const int gw = min(G, ntn - band * G);
-    const int n0 = (band * G + rr0 % gw) * GB, m0 = (rr0 / gw) * GB;
+    n0 = (band * G + rr0 % gw) * GB;
+    m0 = (rr0 / gw) * GB;
+}
 
-    // glds sources: half-tile H, piece i*8 + wave (8 rows of 128 B), lane -> row, swizzled chunk
+// glds source of half-tile H (0, 1: A rows m0 + 128 H; 2, 3: W rows n0 + 128 (H - 2)),
+// piece i*8 + wave (8 rows of 128 B), lane -> row, swizzled chunk
+__device__ __forceinline__ const h16* src8p(const GemmArgs& g, int m0, int n0, int H, int i, int wave, int lane) {
+    const int rr = (i * 8 + wave) * 8 + (lane >> 3);
+    const int c = swz(rr, lane & 7);
+    const int hh = H & 1;
+    if (H < 2) return grp_row(g.A, min(m0 + hh * 128 + rr, g.M - 1), g.a_grp_rows, g.a_grp_stride, g.lda) + c * 8;
+    return g.W + (int64_t)min(n0 + hh * 128 + rr, g.N - 1) * g.ldw + c * 8;
+}
+
+__device__ __forceinline__ void lds_sync() {  // LDS accesses of every wave done, vmcnt untouched
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// The persistent 8-phase kernel's epilogue when the next tile's first K-tile is already
+// in flight into ring buffer 0 (NEXT0): the image lives in buffer 1 (the upper 64 KiB) and
+// the tile leaves in passes that fit it — fp16: two 128-row halves, fp32: four 64-row
+// quarters — with LDS-only barriers, so the prefetch loads stay in flight throughout.
+template <int EPI>
+__device__ __forceinline__ void staged_epilogue_next0(const GemmArgs& g, f32x4 (&acc)[8][4], int m0, int n0, int wm,
+                                                      int wn, char* smem, int tid) {
+    const int lane = tid & 63;
+    constexpr bool F16 = EPI == EPI_F16 || EPI == EPI_F16_GELU || EPI == EPI_HEADS;
+    constexpr int PR = F16 ? 128 : 64;       // image rows per pass
+    constexpr int NP = 256 / PR;
+    lds_sync();  // every wave is past its last read of buffer 1 (the last K-tile's)
+#pragma unroll
+    for (int pass = 0; pass < NP; ++pass) {
+        if constexpr (F16) {
+            h16* T = (h16*)(smem + 4 * HT * 2);
+#pragma unroll
+            for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        if ((mi >> 2) != pass) continue;
+                        const int row = acc_row<true>(wm, mi) - pass * PR + (lane >> 4) * 4 + i;
+                        const int col = acc_col<true>(wn, ni) + (lane & 15);
+                        const int n = min(n0 + col, g.N - 1);
+                        T[ep16(row, col)] = (h16)epi_value<EPI>(g, m0 + pass * PR + row, n, acc[mi][ni][i]);
+                    }
+            lds_sync();
+#pragma unroll 4
+            for (int j = 0; j < 8; ++j) {
+                const int id = j * GNT + tid;
+                const int row = id >> 5, c8 = (id & 31) * 8;
+                const int m = m0 + pass * PR + row, n = n0 + c8;
+                if (m >= g.M || n >= g.N) continue;
+                const h16x8 v = *(const h16x8*)&T[ep16(row, c8)];
+                h16* dst;
+                if constexpr (EPI == EPI_HEADS) {
+                    const int D = g.heads_H * 64;
+                    const int which = n / D, h = (n % D) >> 6, d = n & 63;
+                    const int b = m / g.heads_T, t = m % g.heads_T;
+                    dst = (h16*)g.C + ((((int64_t)which * g.heads_nb + b) * g.heads_H + h) * g.heads_T + t) * 64 + d;
+                } else {
+                    dst = (h16*)g.C + (m / g.c_grp_rows) * g.c_grp_stride + (int64_t)(m % g.c_grp_rows) * g.ldc + n;
+                }
+                __builtin_nontemporal_store(v, (h16x8*)dst);
+            }
+        } else {
+            float* T = (float*)(smem + 4 * HT * 2);
+            // pass p = rows [64 p, 64 p + 64): wave rows (mi >> 2) * 128 + wm * 64
+            if (wm == (pass & 1)) {
+#pragma unroll
+                for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            if ((mi >> 2) != (pass >> 1)) continue;
+                            const int row = acc_row<true>(wm, mi) - pass * PR + (lane >> 4) * 4 + i;
+                            const int col = acc_col<true>(wn, ni) + (lane & 15);
+                            const int n = min(n0 + col, g.N - 1);
+                            T[ep32(row, col)] = epi_value<EPI>(g, m0 + pass * PR + row, n, acc[mi][ni][i]);
+                        }
+            }
+            lds_sync();
+#pragma unroll 4
+            for (int j = 0; j < 8; ++j) {
+                const int id = j * GNT + tid;
+                const int row = id >> 6, c4 = (id & 63) * 4;
+                const int m = m0 + pass * PR + row, n = n0 + c4;
+                if (m < g.M && n < g.N) {
+                    f32x4 v = *(const f32x4*)&T[ep32(row, c4)];
+                    float* dst = (float*)g.C + (m / g.c_grp_rows) * g.c_grp_stride + (int64_t)(m % g.c_grp_rows) * g.ldc + n;
+                    if constexpr (EPI == EPI_F32_RESID) v += *(const f32x4*)dst;
+                    if constexpr (EPI == EPI_F32_GELU_POS) {
+                        const f32x4 pv = *(const f32x4*)&g.pos[(int64_t)(m % g.c_grp_rows) * g.N + n];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]) + pv[e];
+                    }
+                    __builtin_nontemporal_store(v, (f32x4*)dst);
+                }
+            }
+        }
+        lds_sync();  // the image's reads are done before the next pass (or the next tile) writes it
+    }
+}
+
+// NEXT0: K-tile 0 of this tile was staged by the previous tile (pre0) / stage the next
+// tile's K-tile 0 (next_bid >= 0) before this tile's epilogue
+template <int EPI, bool NOEPI>
+__device__ __forceinline__ void gemm8p_tile(const GemmArgs& g, int bid, h16* smem, int tid, bool pre0 = false,
+                                            int next_bid = -1) {
+    const int wave = tid >> 6, lane = tid & 63;
+    int m0, n0;
+    tile8p_origin(g, bid, m0, n0);
+
     const h16* src[4][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int rr = (i * 8 + wave) * 8 + (lane >> 3);
-        const int c = swz(rr, lane & 7);
+    for (int H = 0; H < 4; ++H)
 #pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-            src[hh][i] = grp_row(g.A, min(m0 + hh * 128 + rr, g.M - 1), g.a_grp_rows, g.a_grp_stride, g.lda) + c * 8;
-            src[2 + hh][i] = g.W + (int64_t)min(n0 + hh * 128 + rr, g.N - 1) * g.ldw + c * 8;
-        }
-    }
+        for (int i = 0; i < 2; ++i) src[H][i] = src8p(g, m0, n0, H, i, wave, lane);
     auto stage = [&](int H, int t) {
         h16* base = smem + ((t & 1) * 4 + H) * HT;
 #pragma unroll
@@ -507,10 +615,12 @@ __device__ __forceinline__ void gemm8p_tile(const GemmArgs& g, int bid, h16* sme
 
     const int nk = g.K / BK;
     // prologue = phases 3, 4 of tile -2 and tile -1 in the steady-state order
-    stage(0, 0);
-    stage(3, 0);
-    stage(1, 0);
-    stage(2, 0);
+    if (!pre0) {
+        stage(0, 0);
+        stage(3, 0);
+        stage(1, 0);
+        stage(2, 0);
+    }
     if (nk > 1) {
         stage(0, 1);
         stage(3, 1);
@@ -556,6 +666,21 @@ __device__ __forceinline__ void gemm8p_tile(const GemmArgs& g, int bid, h16* sme
         barrier();
     }
     if (__builtin_amdgcn_readfirstlane(wave) < 4) barrier();
+    if (next_bid >= 0) {
+        // every wave is past its reads of buffer 0 (the last K-tile read buffer 1: nk even):
+        // the next tile's K-tile 0 streams in while this tile's epilogue runs in buffer 1
+        lds_sync();
+        int nm0, nn0;
+        tile8p_origin(g, next_bid, nm0, nn0);
+#pragma unroll
+        for (int H : {0, 3, 1, 2})
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                __builtin_amdgcn_global_load_lds((const void*)src8p(g, nm0, nn0, H, i, wave, lane),
+                                                 (OSW_LDS void*)(smem + H * HT + (i * 8 + wave) * 8 * BK), 16, 0, 0);
+        if constexpr (!NOEPI) staged_epilogue_next0<EPI>(g, acc, m0, n0, wm, wn, (char*)smem, tid);
+        return;
+    }
     if constexpr (NOEPI) {
         float t = 0.f;
 #pragma unroll
@@ -580,14 +705,20 @@ template <int EPI, bool NOEPI = false>  // NOEPI: no epilogue (debug variant 9: 
 __global__ __launch_bounds__(GNT, 1) void gemm8p_kernel(GemmArgs g) {
     extern __shared__ __attribute__((aligned(16))) h16 smem[];  // [2][A0 A1 W0 W1][128*64]
     const int nwg = ((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
+    // next0 (g.kc bit, see launch8p): the next tile's first K-tile is staged before this
+    // tile's epilogue (needs an even K-tile count: the last K-tile then sits in buffer 1)
+    const bool next0 = g.kc == 1 && (g.K / BK) % 2 == 0;
+    bool pre0 = false;
     for (int vb = blockIdx.x; vb < nwg; vb += gridDim.x) {
         // the thread id passes through an opaque move each tile, so nothing derived from it
         // (fragment offsets, staging addresses) is hoisted out of the loop and kept live
         // across tiles: the one-tile body already needs ~206 VGPRs (hoisted: 256 + spills)
         int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
-        gemm8p_tile<EPI, NOEPI>(g, vb, smem, tid);
-        __syncthreads();  // the epilogue's LDS image is the next tile's operand ring
+        const int nxt = next0 && vb + (int)gridDim.x < nwg ? vb + (int)gridDim.x : -1;
+        gemm8p_tile<EPI, NOEPI>(g, vb, smem, tid, pre0, nxt);
+        pre0 = nxt >= 0;
+        if (!pre0) __syncthreads();  // the epilogue's LDS image is the next tile's operand ring
     }
 }
 
@@ -602,6 +733,11 @@ void launch8p(const GemmArgs& g0, hipStream_t s) {
     }
     GemmArgs g = g0;
     g.band = choose_band(g);
+    static const bool next0 = [] {  // OSW_GEMM_NEXT0=0: the epilogue and the next tile's fill do not overlap
+        const char* e = std::getenv("OSW_GEMM_NEXT0");
+        return !(e && e[0] == '0');
+    }();
+    g.kc = next0 ? 1 : 0;  // (kc is unused by the 8-phase kernel otherwise)
     const int nwg = ((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
     static const int grid_cap = [] {
         const char* e = std::getenv("OSW_GEMM_PERSIST");  // 0: one workgroup per tile
@@ -609,6 +745,8 @@ void launch8p(const GemmArgs& g0, hipStream_t s) {
         int dev = 0, cus = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             return 1 << 30;
+        // OSW_GEMM_GRID=n: at most n workgroups (A/B: leave CUs to another lane's decoder)
+        if (const char* gg = std::getenv("OSW_GEMM_GRID")) return std::max(8, std::min(cus, atoi(gg)) / 8 * 8);
         return cus / 8 * 8;  // one workgroup per CU, a multiple of the 8 XCDs
     }();
     gemm8p_kernel<EPI, NOEPI><<<std::min(nwg, std::max(8, grid_cap)), GNT, lds, s>>>(g);
@@ -724,7 +862,101 @@ __global__ __launch_bounds__(NTHR, 2) void gemm64_ring_kernel(GemmArgs g) {
         }
 }
 
-template <int MT, bool DIRECT, int EPI, bool LO, int PRO = PRO_NONE>
+__device__ __forceinline__ void sel_merge(SelPart& r, const SelPart& q) {
+    lse_merge(r.m_all, r.s_all, q.m_all, q.s_all);
+    lse_merge(r.m_ts, r.s_ts, q.m_ts, q.s_ts);
+    const ArgMax A = amax(ArgMax{r.v_all, r.i_all}, ArgMax{q.v_all, q.i_all});
+    const ArgMax X = amax(ArgMax{r.v_text, r.i_text}, ArgMax{q.v_text, q.i_text});
+    const ArgMax T = amax(ArgMax{r.v_ts, r.i_ts}, ArgMax{q.v_ts, q.i_ts});
+    r.v_all = A.v; r.i_all = A.i; r.v_text = X.v; r.i_text = X.i; r.v_ts = T.v; r.i_ts = T.i;
+}
+
+__device__ __forceinline__ SelPart sel_xor(const SelPart& r, int o) {
+    SelPart q;
+    switch (o) {  // xor_lane needs a compile-time offset
+#define OSW_SX(O) case O: q = SelPart{xor_lane<O>(r.m_all), xor_lane<O>(r.s_all), xor_lane<O>(r.m_ts), \
+                                      xor_lane<O>(r.s_ts), xor_lane<O>(r.v_all), xor_lane<O>(r.v_text), \
+                                      xor_lane<O>(r.v_ts), xor_lane<O>(r.i_all), xor_lane<O>(r.i_text), \
+                                      xor_lane<O>(r.i_ts)}; break;
+        OSW_SX(32) OSW_SX(16) OSW_SX(8) OSW_SX(4) OSW_SX(2) default: OSW_SX(1)
+#undef OSW_SX
+    }
+    return q;
+}
+
+// A workgroup's SelPart over 64 lanes x 4 waves (fixed merge pattern), in thread 0.
+__device__ __forceinline__ SelPart sel_block_merge(SelPart r, SelPart* wp) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const SelPart q = sel_xor(r, o);
+        sel_merge(r, q);
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) wp[w] = r;
+    __syncthreads();
+    SelPart t = wp[0];
+    for (int i = 1; i < 4; ++i) sel_merge(t, wp[i]);
+    return t;
+}
+
+// The selection of select_kernel (greedy, one row) on the logits this workgroup just
+// computed: lane `valid` holds logit x of vocabulary entry `col`.  Entries are folded
+// into the slice statistics exactly as select_partial_body does; the workgroup's record
+// goes to parts[blockIdx.x] and the last workgroup to arrive merges all records in
+// workgroup order, finalises the row and advances the step counter.
+__device__ __forceinline__ void fused_select_row(float x, int col, bool valid, const SelFuse& F) {
+    __shared__ SelPart wp[4];
+    __shared__ int last;
+    const SelParams& P = F.P;
+    const int step = *F.pos;
+    const SelState s = F.st[0];
+    const int mode = sel_mode(P, step, s);
+    const SelPart id{-INFINITY, 0.f, -INFINITY, 0.f, -INFINITY, -INFINITY, -INFINITY, 0x7fffffff, 0x7fffffff,
+                     0x7fffffff};
+    SelPart r = id;
+    if (valid && (mode == SEL_SOT || mode == SEL_SAMPLE)) {
+        ArgMax a_all{-INFINITY, 0x7fffffff}, a_text{-INFINITY, 0x7fffffff}, a_ts{-INFINITY, 0x7fffffff};
+        const int v = col;
+        if (mode == SEL_SOT) {
+            lse_add(r.m_all, r.s_all, x);
+            if (v >= P.first_lang && v < P.first_lang + P.n_langs) a_text = ArgMax{x, v};
+        } else if (!tok_masked_w(P, row_rules(P, s), F.supmask[v >> 5], v)) {
+            lse_add(r.m_all, r.s_all, x);
+            a_all = ArgMax{x, v};
+            if (v >= P.tb) {
+                lse_add(r.m_ts, r.s_ts, x);
+                a_ts = ArgMax{x, v};
+            } else {
+                a_text = ArgMax{x, v};
+            }
+        }
+        r.v_all = a_all.v; r.i_all = a_all.i; r.v_text = a_text.v; r.i_text = a_text.i; r.v_ts = a_ts.v; r.i_ts = a_ts.i;
+    }
+    SelPart* parts = (SelPart*)F.parts;
+    const int nwg = gridDim.x;
+    r = sel_block_merge(r, wp);
+    if (threadIdx.x == 0) {
+        store_part(parts + blockIdx.x, r);
+        __builtin_amdgcn_s_waitcnt(0);  // the record is complete at device scope before the ticket
+        last = __hip_atomic_fetch_add(F.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nwg - 1;
+        if (last) __hip_atomic_store(F.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last) return;
+    SelPart t = id;
+    for (int i = threadIdx.x; i < nwg; i += 256) sel_merge(t, load_part(parts + i));
+    __syncthreads();  // wp is reused
+    t = sel_block_merge(t, wp);
+    if (threadIdx.x != 0) return;
+    // the logits the finaliser reads back (no-speech prob, an <|endoftext|> log-prob) were
+    // stored by other workgroups of this launch: write-through stores, device-scope loads
+    select_finalize<true>(F.logits, P, step, F.prompt, [&] { return t; }, F.st, F.cur_tok, F.tokens, F.max_tokens,
+                          0);
+    __builtin_amdgcn_s_waitcnt(0);
+    __hip_atomic_store(F.pos, step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int MT, bool DIRECT, int EPI, bool LO, int PRO = PRO_NONE, bool SEL = false>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, float* __restrict__ part, ProArgs pa) {
     // Workgroup = 64 columns x one kc-deep K range; wave = 16 columns.  The
     // activation rows (M <= 64) of each CKK-deep K chunk are staged ONCE per
@@ -764,9 +996,21 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
     __shared__ __attribute__((aligned(16))) h16 Ap[PRO ? 2 : 1][APR][APS];
     __shared__ float pred[PRO ? 2 * PRO_ROWS * 4 : 1];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int nb = blockIdx.x * 64 + wave * 16;
-    const int ks = blockIdx.y;
-    const int mb = blockIdx.z * ROWS;  // row group (partial mode, M > 64: beam rows)
+    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    if (g.pair_rows) {
+        // 1-D grid: workgroup id = 8 j + xcd, j = unit * nz + row group, unit = (column
+        // block, K range) numbered xcd-major: every row group of a unit on one XCD, adjacent
+        const int nz = (g.M + ROWS - 1) / ROWS, gx = (g.N + 63) / 64, units = gx * (g.K / kc);
+        const int j = blockIdx.x >> 3;
+        const int u = (j / nz) * 8 + (blockIdx.x & 7);
+        if (u >= units) return;
+        bz = j % nz;
+        bx = u % gx;
+        by = u / gx;
+    }
+    const int nb = bx * 64 + wave * 16;
+    const int ks = by;
+    const int mb = bz * ROWS;  // row group (partial mode, M > 64: beam rows)
     const int k0 = ks * kc;
     const int n = min(nb + (lane & 15), g.N - 1);
     const h16* wrow = g.W + (int64_t)n * g.ldw + k0 + 8 * (lane >> 4);
@@ -840,6 +1084,37 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
         }
     };
     constexpr int INFLIGHT = CK + (PRO ? 0 : NIMG * APIECES);  // one chunk's loads per lane
+    // 32-row hi/lo groups stream 64-deep chunks (CK = 2): one chunk of weights ahead is
+    // 8 KB in flight per workgroup, so the 32 KB of a 256-deep K range took ~4 dependent
+    // HBM round trips.  With preload_w every k32 step's weights (8 x 16 B per lane, 32
+    // VGPRs) is issued at the start: one round trip, the A chunks staged behind it.
+    if constexpr (PRO == PRO_NONE && CK < 8) {
+        constexpr int WALL = 8;
+        if (g.preload_w && nsteps <= WALL) {
+            constexpr int AL = NIMG * APIECES;   // LDS-DMA loads per lane per chunk
+            h16x8 w[WALL];
+#pragma unroll
+            for (int u = 0; u < WALL; ++u) w[u] = *(const h16x8*)(wrow + 32 * min(u, nsteps - 1));
+            stageA(0, 0);
+            if (nch > 1) stageA(1, 1);
+#pragma unroll
+            for (int c = 0; c < WALL / CK; ++c) {
+                if (c >= nch) break;
+                if (c + 1 < nch) wait_vmcnt<AL>();   // chunk c's A landed (and every weight load)
+                else wait_vmcnt<0>();
+                __builtin_amdgcn_s_barrier();
+                h16x8 wf[CK];
+#pragma unroll
+                for (int u = 0; u < CK; ++u) wf[u] = w[c * CK + u];
+                consume(wf, c & 1, c);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                if (c + 2 < nch) stageA(c & 1, c + 2);
+            }
+            goto store;
+        }
+    }
+    {
     h16x8 wa[CK], wb[CK];
     loadW(wa, 0);
     stageA(0, 0);
@@ -901,7 +1176,16 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
     }
+    }
+store:
     const int col = nb + li;
+    if constexpr (SEL) {
+        static_assert(MT == 1 && DIRECT, "the fused selection serves the batch-1 logits GEMM");
+        const bool valid = gq == 0 && col < g.N;
+        if (valid) __hip_atomic_store((float*)g.C + col, acc[0][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fused_select_row(acc[0][0], col, valid, pa.sel);
+        return;
+    }
     if (col >= g.N) return;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
@@ -1131,10 +1415,18 @@ int skinny_ksplit(int N, int K) {
 // Hi/lo rows beyond 32 run as 32-row groups (MT = 2, 16 KiB of LDS): a 64-row workgroup
 // (32 KiB) cannot start beside another lane's encoder GEMM tile, and the decoder then
 // stalled for whole encoder tiles (51 us per projection instead of 16).
-int launch_gemm_skinny_partial(const GemmArgs& g, float* part, hipStream_t s) {
+int launch_gemm_skinny_partial(const GemmArgs& g0, float* part, hipStream_t s) {
+    static const bool no_pre = getenv("OSW_SKINNY_NOPRE") != nullptr;    // A/B switches
+    static const bool no_pair = getenv("OSW_SKINNY_NOPAIR") != nullptr;
+    GemmArgs g = g0;
+    g.preload_w = no_pre ? 0 : 1;
     const int ks = skinny_ksplit(g.N, g.K);
     const int gr = (g.A_lo && g.M > 32) ? 32 : 64;
-    const dim3 grid((g.N + 63) / 64, ks, (g.M + gr - 1) / gr);
+    const int nz = (g.M + gr - 1) / gr;
+    g.pair_rows = (nz > 1 && !no_pair) ? 1 : 0;
+    const int units = (g.N + 63) / 64 * ks;
+    const dim3 grid = g.pair_rows ? dim3((unsigned)(8 * ((units + 7) / 8) * nz), 1, 1)
+                                  : dim3((g.N + 63) / 64, ks, nz);
     const int kc = g.K / ks;
 #define OSW_SKINNY_PART(MT_)                                                                     \
     do {                                                                                         \
@@ -1159,12 +1451,19 @@ int launch_gemm_skinny_partial(const GemmArgs& g, float* part, hipStream_t s) {
 // Fused small-batch form (<= PRO_ROWS hi/lo rows for PRO_RESLN, <= GELU_ROWS for PRO_GELU):
 // the operand is built by the prologue (resln.h).  direct: one K range, EPI_F32 straight into g.C (the logits); otherwise the
 // split-K slabs into part, as launch_gemm_skinny_partial.  Returns ksplit.
-int launch_gemm_skinny_pro(const GemmArgs& g, int pro, const ProArgs& pa, bool direct, float* part, hipStream_t s) {
+int launch_gemm_skinny_pro(const GemmArgs& g, int pro, const ProArgs& pa, bool direct, float* part, hipStream_t s,
+                           bool select) {
     const int ks = direct ? 1 : skinny_ksplit(g.N, g.K);
     const dim3 grid((g.N + 63) / 64, ks, 1);
     const int kc = g.K / ks;
     if (pro == PRO_GELU ? g.M > GELU_ROWS || kc > GELU_KC : g.M > PRO_ROWS)
         throw std::invalid_argument("fused GEMM prologue: rows or K range exceed its LDS image");
+    if (select) {
+        if (!direct || pro != PRO_RESLN || g.M != 1 || g.epi != EPI_F32 || g.ldc != g.N)
+            throw std::invalid_argument("fused selection: batch-1 logits GEMM only");
+        gemm_skinny_kernel<1, true, EPI_F32, true, PRO_RESLN, true><<<grid, 256, 0, s>>>(g, kc, part, pa);
+        return ks;
+    }
     if (direct) {
         if (pro == PRO_RESLN) gemm_skinny_kernel<1, true, EPI_F32, true, PRO_RESLN><<<grid, 256, 0, s>>>(g, kc, part, pa);
         else gemm_skinny_kernel<1, true, EPI_F32, true, PRO_GELU><<<grid, 256, 0, s>>>(g, kc, part, pa);

@@ -209,6 +209,7 @@ struct osw_ctx {
     unsigned* supmask = nullptr;
     SelState* sel = nullptr;   // per decoder row
     void* selp = nullptr;      // per-row vocabulary-slice partial stats
+    void* selp1 = nullptr;     // batch-1 fused selection: one record per logits workgroup
     int* anc = nullptr;        // beam: [R][ctx] row whose cache slot holds position p of this hypothesis
     int* btok = nullptr;       // beam: [B][ctx] best finished hypothesis per window
     BeamWin* bwin = nullptr;   // beam: [B]
@@ -488,6 +489,7 @@ void setup_workspace(osw_ctx* c) {
     c->supmask = dalloc<unsigned>((d.n_vocab + 31) / 32, o);
     c->sel = dalloc<SelState>(R, o);
     c->selp = dalloc<char>((size_t)R * sel_parts_bytes(), o);
+    c->selp1 = dalloc<char>((size_t)sel_fused_parts_bytes(d.n_vocab), o);
     c->anc = dalloc<int>(R * d.n_text_ctx, o);
     c->btok = dalloc<int>(B * d.n_text_ctx, o);
     c->bwin = dalloc<BeamWin>(B, o);
@@ -656,7 +658,7 @@ void encode(osw_ctx* c, const osw_window* wins, int n) {
 // ping-pongs between xd and xd2 (every workgroup of a GEMM reads x, one writes x'), the
 // slabs between part and part2 (a GEMM's prologue reads its producer's slabs while its
 // epilogue writes its own).  Same arithmetic as decoder_step's separate kernels.
-void decoder_step_fused(osw_ctx* c, int nb, int group, bool gather) {
+void decoder_step_fused(osw_ctx* c, int nb, int group, bool gather, const SelFuse* sf) {
     const osw_dims& d = c->d;
     const int D = d.n_text_state, H = d.n_text_head, L = d.n_text_layer, ctx = d.n_text_ctx;
     const int64_t xkv_which = (int64_t)(nb / group) * H * T_ENC * 64;
@@ -712,8 +714,9 @@ void decoder_step_fused(osw_ctx* c, int nb, int group, bool gather) {
     GemmArgs gl = gemm(nullptr, WH(c, "dec.tok"), d.n_vocab, D);
     gl.C = c->logits;
     gl.ldc = d.n_vocab;
-    launch_gemm_skinny_pro(gl, PRO_RESLN, resln(WF(c, pl + ".fc2.b"), "dec.lnpost", false), true, nullptr,
-                           c->stream);
+    ProArgs pl_args = resln(WF(c, pl + ".fc2.b"), "dec.lnpost", false);
+    if (sf) pl_args.sel = *sf;
+    launch_gemm_skinny_pro(gl, PRO_RESLN, pl_args, true, nullptr, c->stream, sf != nullptr);
     HIPCHK(hipGetLastError());
 }
 
@@ -723,7 +726,9 @@ void decoder_step_fused(osw_ctx* c, int nb, int group, bool gather) {
 // nb = decoder rows (windows x group); the `group` rows of one window are adjacent
 // (beam hypotheses or best_of samples); `gather` = beam rows read the self-K/V cache
 // through the ancestry table.
-void decoder_step(osw_ctx* c, int nb, int group, bool gather) {
+// sf (batch-1 greedy): the logits GEMM also selects the token and advances the step
+// counter; returns whether it did (the caller then launches no select).
+bool decoder_step(osw_ctx* c, int nb, int group, bool gather, const SelFuse* sf = nullptr) {
     const osw_dims& d = c->d;
     const int D = d.n_text_state, H = d.n_text_head, L = d.n_text_layer, ctx = d.n_text_ctx;
     const int64_t xkv_which = (int64_t)(nb / group) * H * T_ENC * 64;
@@ -754,8 +759,8 @@ void decoder_step(osw_ctx* c, int nb, int group, bool gather) {
     };
     static const bool no_fuse = getenv("OSW_NO_FUSE") != nullptr;  // A/B switch
     if (nb <= PRO_ROWS && !no_fuse) {
-        decoder_step_fused(c, nb, group, gather);
-        return;
+        decoder_step_fused(c, nb, group, gather, nb == 1 ? sf : nullptr);
+        return sf != nullptr && nb == 1;
     }
     static const bool no_gelu_pro = getenv("OSW_NO_GELU_PRO") != nullptr;  // A/B switch
     const bool gelu_pro = nb <= GELU_ROWS && !no_gelu_pro && 4 * D / skinny_ksplit(D, 4 * D) <= GELU_KC;
@@ -803,6 +808,7 @@ void decoder_step(osw_ctx* c, int nb, int group, bool gather) {
     GemmArgs gl = gemm_plain(c->xdn, D, WH(c, "dec.tok"), nullptr, nb, d.n_vocab, D, c->logits, d.n_vocab, EPI_F32);
     gl.A_lo = c->xdn + lo_d;
     run_gemm(c, gl, 0);
+    return false;
 }
 
 void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) {
@@ -886,9 +892,14 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
             launch_beam(c->logits, nb, c->pos, SP, c->supmask, c->sel, c->selp, c->bcand, c->tokens, c->anc,
                         d.n_text_ctx, c->bwin, c->btok, c->cur_tok, max_tok, c->sel_arrive, c->stream);
     };
+    // batch-1 greedy: the selection runs in the logits GEMM's epilogue (SelFuse, decode.h)
+    static const bool no_fuse_sel = getenv("OSW_NO_FUSE_SELECT") != nullptr;  // A/B switch
+    SelFuse sf{SP, c->logits, c->pos, c->supmask, c->prompt, c->sel, c->cur_tok, c->tokens, max_tok, c->selp1,
+               c->sel_arrive + 1};
+    const SelFuse* sfp = (rows == 1 && beam == 1 && !sampling && !no_fuse_sel) ? &sf : nullptr;
     auto one_step = [&] {
-        decoder_step(c, rows, group, beam > 1);
-        select();  // the select kernel (greedy) or the beam update advances the step counter
+        // the select kernel (greedy), the beam update or the fused selection advances the step counter
+        if (!decoder_step(c, rows, group, beam > 1, sfp)) select();
     };
     const int CH = 8;
     const bool graph = c->use_graph && !r->logits_dump && !c->prof_eager;
@@ -948,12 +959,12 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
             } else {
                 const int samp = steps - (P - 1);
                 if (r->logits_dump && samp >= 0 && samp < r->dump_steps) {
-                    decoder_step(c, rows, group, beam > 1);
+                    const bool selected = decoder_step(c, rows, group, beam > 1, sfp);
                     for (int b = 0; b < nb; ++b)
                         HIPCHK(hipMemcpyAsync(r->logits_dump + ((size_t)b * r->dump_steps + samp) * V,
                                               c->logits + (size_t)b * V, (size_t)V * 4, hipMemcpyDeviceToHost,
                                               c->stream));
-                    select();
+                    if (!selected) select();
                 } else {
                     one_step();
                 }

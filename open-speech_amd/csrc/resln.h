@@ -13,6 +13,7 @@
 // wave_sum, then the 4 wave partials in order.
 #pragma once
 #include "common.h"
+#include "decode.h"
 
 namespace osw {
 
@@ -157,6 +158,7 @@ struct ProArgs {
     const float* part;   // PRO_GELU: the fc1 slabs [ks][M][K], K = this GEMM's K
     int ks;
     const float* bias;
+    SelFuse sel;         // the batch-1 logits GEMM with the selection in its epilogue (decode.h)
 };
 
 // fc1 -> fc2 operand: fp16 pair of gelu(bias + Σ_k part[k][r][n]), k in order (the order of

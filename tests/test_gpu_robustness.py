@@ -71,7 +71,8 @@ def nan_engine():
     eng.close()
 
 
-@pytest.mark.parametrize("mode", ["greedy_detect", "greedy_lang", "beam5", "sampling", "greedy_graph_rows"])
+@pytest.mark.parametrize("mode", ["greedy_detect", "greedy_lang", "beam5", "sampling", "greedy_graph_rows",
+                                  "greedy_b1", "greedy_b1_lang"])
 def test_nan_logits_end_rows_without_fault(nan_engine, mode):
     """an all-NaN row never produces a winner (a NaN never beats the argmax
     seed {-inf, INT_MAX}).  Greedy, sampling and the language argmax must end the row
@@ -91,6 +92,10 @@ def test_nan_logits_end_rows_without_fault(nan_engine, mode):
         kw.update(temperature=0.7, best_of=2, seed=3)
     elif mode == "greedy_graph_rows":
         n = 8                      # decode graph (no dump), 8 rows
+    elif mode.startswith("greedy_b1"):
+        n = 1                      # one row: the selection fused into the logits GEMM
+        if mode.endswith("lang"):
+            kw["language_token"] = st.first_lang
     clips = [synth.chirp_clip(70 + i, 30.0) for i in range(n)]
     outs = eng.transcribe_batch(clips, DecodeConfig(**kw))
     for o in outs:
@@ -118,3 +123,38 @@ def test_context_usable_after_nan_rows(nan_engine):
         fresh.close()
     assert got.tokens == want.tokens and got.sum_logprob == want.sum_logprob
     assert all(0 <= t < d.n_vocab for t in got.tokens)
+
+
+def test_batch1_fused_selection_equals_select_kernel():
+    """One decoder row selects its token in the logits GEMM's epilogue (SelFuse); two or
+    more rows use select_kernel.  The same window alone and in a 2-window batch: ids,
+    language and no-speech prob identical, sum_logprob equal up to the order of the
+    log-sum-exp merges (811 workgroup records vs 16 slices); with a token budget (the
+    finaliser's <|endoftext|> read-back) and with the logits dump (eager steps)."""
+    d = D.TINY_TEST
+    w = weights.random_weights(d, seed=1234, emb_std=0.5)
+    eng = WhisperEngine(d, device=0, max_batch=2)
+    try:
+        eng.load_weights(w)
+        sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+        clips = [synth.chirp_clip(90, 30.0), synth.chirp_clip(91, 17.0)]
+        for budget in (None, (7, 11)):
+            cfg = DecodeConfig(suppress_tokens=sup, max_length=96, token_budget=budget)
+            both = eng.transcribe_batch(clips, cfg)
+            for i, c in enumerate(clips):
+                one_cfg = DecodeConfig(suppress_tokens=sup, max_length=96,
+                                       token_budget=None if budget is None else (budget[i],))
+                one = eng.transcribe_batch([c], one_cfg)[0]
+                assert one.tokens == both[i].tokens, (budget, i)
+                assert one.language == both[i].language
+                assert abs(one.no_speech_prob - both[i].no_speech_prob) < 1e-5
+                assert abs(one.sum_logprob - both[i].sum_logprob) <= 1e-4 * (len(one.tokens) + 1)
+                if budget is not None:
+                    assert len(one.tokens) == budget[i]
+        eng.log_mel(clips[:1])
+        eng.encode([(0, 0, 3000)])
+        cfg = DecodeConfig(suppress_tokens=sup, max_length=96)
+        dumped = eng.decode(1, cfg, dump_steps=3)[0]
+        assert dumped.tokens == eng.transcribe_batch(clips[:1], cfg)[0].tokens
+    finally:
+        eng.close()

@@ -143,3 +143,33 @@ def test_kernel_constants_cover_rows():
         for lo in (False, True):
             CK, CKK, CPR, RPP, SWM, ROWS, APIECES = kernel_consts(MT, lo)
             assert APIECES * 4 * RPP == ROWS, (MT, lo)
+
+
+def test_pair_rows_grid_is_a_bijection():
+    """pair_rows (launch_gemm_skinny_partial, > 1 row group): the 1-D grid's workgroups
+    cover every (column block, K range, row group) exactly once, and the row groups of
+    one (column block, K range) share an XCD (workgroup id % 8) with adjacent ids."""
+    for dims in (D.MICRO_TEST, D.TINY_TEST, D.LARGE_V3_TURBO):
+        for M in (33, 64, 65, 128, 320):
+            for N, K in SHAPES(dims.n_text_state):
+                ks, nz, MT = partial_launch(M, N, K, True)
+                if nz == 1:
+                    continue
+                gx = (N + 63) // 64
+                kc = K // ks
+                units = gx * (K // kc)
+                seen = {}
+                for bid in range(8 * ((units + 7) // 8) * nz):
+                    j = bid >> 3
+                    u = (j // nz) * 8 + (bid & 7)
+                    if u >= units:
+                        continue
+                    key = (u % gx, u // gx, j % nz)
+                    assert key not in seen, key
+                    seen[key] = bid
+                assert len(seen) == units * nz
+                for bx in range(gx):
+                    for by in range(ks):
+                        ids = [seen[(bx, by, z)] for z in range(nz)]
+                        assert len({i % 8 for i in ids}) == 1
+                        assert ids == list(range(ids[0], ids[0] + 8 * nz, 8))

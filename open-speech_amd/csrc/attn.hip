@@ -19,6 +19,8 @@
 // Layout out: O [nb*T][H*64] fp16 row-major (the out-projection GEMM's A operand)
 #include "common.h"
 
+#include <cstdlib>
+
 namespace osw {
 
 namespace {
@@ -33,6 +35,12 @@ __device__ __forceinline__ h16x4 ds_read_tr(const h16* p) {
     return __builtin_bit_cast(h16x4, v);
 }
 
+// LAZY: the running max is raised only when a tile's max exceeds it by more than 8 in
+// the scaled base-2 domain (so every p = 2^(s*c - m) <= 2^8, exact in fp32 and in the
+// fp16 P operand); O and l stay relative to the same stale max, so the normalised result
+// is the same softmax, and the 32 O rescale multiplies per tile run only when some lane
+// of the wave raised its max (rare after the first tiles) instead of every tile.
+template <bool LAZY>
 __global__ __launch_bounds__(256, 2) void enc_attn_kernel(const h16* __restrict__ qkv, h16* __restrict__ out,
                                                           int T, int H, int nb) {
     __shared__ __attribute__((aligned(16))) h16 lds[2][2][KB * HD];  // [buf][K|V] 32 KiB
@@ -135,7 +143,14 @@ __global__ __launch_bounds__(256, 2) void enc_attn_kernel(const h16* __restrict_
                 }
             mx = fmaxf(mx, xor_lane<16>(mx));
             mx = fmaxf(mx, xor_lane<32>(mx));
-            const float mnew = fmaxf(mrun[qt], mx);
+            float mnew = fmaxf(mrun[qt], mx);
+            bool rescale = true;
+            if constexpr (LAZY) {
+                // keep the stale max while the tile stays within 2^8 of it (the first tile
+                // always takes its max: mrun starts at -inf)
+                if ((mnew - mrun[qt]) * cs <= 8.0f) mnew = mrun[qt];
+                rescale = __any(mnew != mrun[qt]);
+            }
             const float alpha = __builtin_amdgcn_exp2f((mrun[qt] - mnew) * cs);
             mrun[qt] = mnew;
             const float mcs = -mnew * cs;
@@ -149,8 +164,10 @@ __global__ __launch_bounds__(256, 2) void enc_attn_kernel(const h16* __restrict_
                     ls += p[t][i];
                 }
             lrun[qt] = lrun[qt] * alpha + ls;
+            if (rescale) {
 #pragma unroll
-            for (int dt = 0; dt < 4; ++dt) o[qt][dt] *= alpha;
+                for (int dt = 0; dt < 4; ++dt) o[qt][dt] *= alpha;
+            }
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
                 h16x8 f;
@@ -216,7 +233,12 @@ __global__ __launch_bounds__(256, 2) void enc_attn_kernel(const h16* __restrict_
 
 void launch_enc_attn(const h16* qkv, h16* out, int T, int H, int nb, hipStream_t s) {
     dim3 grid((T + QB - 1) / QB, H, nb);
-    enc_attn_kernel<<<grid, 256, 0, s>>>(qkv, out, T, H, nb);
+    static const bool eager = [] {  // OSW_ATTN_LAZY=0: rescale O on every tile (A/B)
+        const char* e = std::getenv("OSW_ATTN_LAZY");
+        return e && e[0] == '0';
+    }();
+    if (eager) enc_attn_kernel<false><<<grid, 256, 0, s>>>(qkv, out, T, H, nb);
+    else enc_attn_kernel<true><<<grid, 256, 0, s>>>(qkv, out, T, H, nb);
 }
 
 }  // namespace osw

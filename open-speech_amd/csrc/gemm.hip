@@ -733,10 +733,15 @@ void launch8p(const GemmArgs& g0, hipStream_t s) {
     }
     GemmArgs g = g0;
     g.band = choose_band(g);
-    static const bool next0 = [] {  // OSW_GEMM_NEXT0=0: the epilogue and the next tile's fill do not overlap
+    // the next tile's first K-tile staged during the epilogue: only the head-major qkv
+    // epilogue gains (1054 -> 1027 us per launch at 64 windows); the fp32 epilogues in four
+    // 64-row passes (o, fc2: 886 -> 956 us) and the GELU one (1485 -> 1535 us) lose, measured.
+    // OSW_GEMM_NEXT0=0: never, =1: every epilogue.
+    static const int next0_env = [] {
         const char* e = std::getenv("OSW_GEMM_NEXT0");
-        return !(e && e[0] == '0');
+        return e ? (e[0] == '1' ? 1 : 0) : -1;
     }();
+    const bool next0 = next0_env < 0 ? EPI == EPI_HEADS : next0_env == 1;
     g.kc = next0 ? 1 : 0;  // (kc is unused by the 8-phase kernel otherwise)
     const int nwg = ((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
     static const int grid_cap = [] {
@@ -745,9 +750,13 @@ void launch8p(const GemmArgs& g0, hipStream_t s) {
         int dev = 0, cus = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             return 1 << 30;
-        // OSW_GEMM_GRID=n: at most n workgroups (A/B: leave CUs to another lane's decoder)
+        // OSW_GEMM_GRID=n: at most n workgroups
         if (const char* gg = std::getenv("OSW_GEMM_GRID")) return std::max(8, std::min(cus, atoi(gg)) / 8 * 8);
-        return cus / 8 * 8;  // one workgroup per CU, a multiple of the 8 XCDs
+        // one workgroup per CU on 3/4 of the CUs (a multiple of the 8 XCDs): the other quarter
+        // never holds an encoder workgroup, so another lane's decoder kernels run there at full
+        // occupancy while this GEMM runs (256 CUs: 192 workgroups, 4768 -> 4872 audio-s/s;
+        // 224: 4864, 160: 4855, measured)
+        return std::max(8, cus * 3 / 4 / 8 * 8);
     }();
     gemm8p_kernel<EPI, NOEPI><<<std::min(nwg, std::max(8, grid_cap)), GNT, lds, s>>>(g);
 }
@@ -943,8 +952,17 @@ __device__ __forceinline__ void fused_select_row(float x, int col, bool valid, c
     }
     __syncthreads();
     if (!last) return;
+    // every record this thread merges is loaded before any is merged: one round trip for
+    // the <= 4 records per thread (811 workgroups at turbo), not one per record
+    constexpr int RPT = 4;
+    SelPart rec[RPT];
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) rec[j] = load_part(parts + min((int)threadIdx.x + 256 * j, nwg - 1));
     SelPart t = id;
-    for (int i = threadIdx.x; i < nwg; i += 256) sel_merge(t, load_part(parts + i));
+#pragma unroll
+    for (int j = 0; j < RPT; ++j)
+        if ((int)threadIdx.x + 256 * j < nwg) sel_merge(t, rec[j]);
+    for (int i = threadIdx.x + 256 * RPT; i < nwg; i += 256) sel_merge(t, load_part(parts + i));
     __syncthreads();  // wp is reused
     t = sel_block_merge(t, wp);
     if (threadIdx.x != 0) return;

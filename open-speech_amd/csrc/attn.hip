@@ -19,6 +19,7 @@
 // Layout out: O [nb*T][H*64] fp16 row-major (the out-projection GEMM's A operand)
 #include "common.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace osw {
@@ -41,17 +42,13 @@ __device__ __forceinline__ h16x4 ds_read_tr(const h16* p) {
 // is the same softmax, and the 32 O rescale multiplies per tile run only when some lane
 // of the wave raised its max (rare after the first tiles) instead of every tile.
 template <bool LAZY>
-__global__ __launch_bounds__(256, 2) void enc_attn_kernel(const h16* __restrict__ qkv, h16* __restrict__ out,
-                                                          int T, int H, int nb) {
-    __shared__ __attribute__((aligned(16))) h16 lds[2][2][KB * HD];  // [buf][K|V] 32 KiB
+__device__ __forceinline__ void enc_attn_unit(const h16* __restrict__ qkv, h16* __restrict__ out, int T, int H,
+                                              int nb, int nqb, int nwg, int bid, h16 (&lds)[2][2][KB * HD]) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g = lane >> 4, li = lane & 15;
     // XCD-aware order: the dispatcher deals workgroups round-robin over 8 XCDs; remap
     // (bijectively) so each XCD walks a contiguous run of (q-block, head, window)
     // indices with the q-block fastest -> one head's K/V stays in one XCD's L2.
-    const int nqb = gridDim.x;
-    const int nwg = nqb * gridDim.y * gridDim.z;
-    const int bid = blockIdx.x + nqb * (blockIdx.y + gridDim.y * blockIdx.z);
     const int qq = nwg / 8, rr = nwg % 8, xcd = bid % 8;
     const int lin = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + bid / 8;
     const int qb = lin % nqb, h = (lin / nqb) % H, b = lin / (nqb * H);
@@ -229,16 +226,39 @@ __global__ __launch_bounds__(256, 2) void enc_attn_kernel(const h16* __restrict_
         }
     }
 }
+
+// Persistent over the (q-block, head, window) units when the grid is capped (workgroup b
+// runs units b, b + grid, ...; grid a multiple of 8, so a unit keeps its XCD): like the
+// encoder GEMM, the attention then leaves a quarter of the CUs to another lane's decoder.
+template <bool LAZY>
+__global__ __launch_bounds__(256, 2) void enc_attn_kernel(const h16* __restrict__ qkv, h16* __restrict__ out,
+                                                          int T, int H, int nb, int nqb) {
+    __shared__ __attribute__((aligned(16))) h16 lds[2][2][KB * HD];  // [buf][K|V] 32 KiB
+    const int nwg = nqb * H * nb;
+    for (int vb = blockIdx.x; vb < nwg; vb += gridDim.x) {
+        enc_attn_unit<LAZY>(qkv, out, T, H, nb, nqb, nwg, vb, lds);
+        __syncthreads();  // the LDS ring is the next unit's
+    }
+}
 }  // namespace
 
 void launch_enc_attn(const h16* qkv, h16* out, int T, int H, int nb, hipStream_t s) {
-    dim3 grid((T + QB - 1) / QB, H, nb);
+    const int nqb = (T + QB - 1) / QB;
+    const int nwg = nqb * H * nb;
     static const bool eager = [] {  // OSW_ATTN_LAZY=0: rescale O on every tile (A/B)
         const char* e = std::getenv("OSW_ATTN_LAZY");
         return e && e[0] == '0';
     }();
-    if (eager) enc_attn_kernel<false><<<grid, 256, 0, s>>>(qkv, out, T, H, nb);
-    else enc_attn_kernel<true><<<grid, 256, 0, s>>>(qkv, out, T, H, nb);
+    // optional grid cap (OSW_ATTN_GRID, A/B only): a capped grid loops over the units.  Default
+    // one workgroup per unit: capping at 2 WGs/CU on 3/4 of the CUs (as the GEMM) measured
+    // 4843/4814 vs 4858/4853 audio-s/s uncapped, 256 and 512 both ~4810 (profiles r03_i).
+    static const int cap = [] {
+        if (const char* e = std::getenv("OSW_ATTN_GRID")) return std::max(8, atoi(e) / 8 * 8);
+        return 1 << 30;
+    }();
+    const int grid = std::min(nwg, cap);
+    if (eager) enc_attn_kernel<false><<<grid, 256, 0, s>>>(qkv, out, T, H, nb, nqb);
+    else enc_attn_kernel<true><<<grid, 256, 0, s>>>(qkv, out, T, H, nb, nqb);
 }
 
 }  // namespace osw

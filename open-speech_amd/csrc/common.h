@@ -128,6 +128,9 @@ struct GemmArgs {
     // block, K range) are consecutive workgroups of one XCD (ids 8j + x, j = row group
     // fastest), so the second group's weight reads hit the L2 the first one filled
     int pair_rows;
+    // 8-phase persistent GEMM: 1 = leave a quarter of the CUs to other lanes' kernels (set
+    // while sibling contexts have calls in flight), 0 = one workgroup on every CU
+    int share_cus;
 };
 
 // fp32 -> (hi, lo) fp16 pair: hi = fp16(v), lo = fp16(v - hi)

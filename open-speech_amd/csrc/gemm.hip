@@ -744,13 +744,18 @@ void launch8p(const GemmArgs& g0, hipStream_t s) {
     const bool next0 = next0_env < 0 ? EPI == EPI_HEADS : next0_env == 1;
     g.kc = next0 ? 1 : 0;  // (kc is unused by the 8-phase kernel otherwise)
     const int nwg = ((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
-    static const int grid_cap = [] {
-        const char* e = std::getenv("OSW_GEMM_PERSIST");  // 0: one workgroup per tile
-        if (e && e[0] == '0') return 1 << 30;
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    static const int cus = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             return 1 << 30;
-        // OSW_GEMM_GRID=n: at most n workgroups
+        return n;
+    }();
+    static const bool per_tile = [] {  // OSW_GEMM_PERSIST=0: one workgroup per tile
+        const char* e = std::getenv("OSW_GEMM_PERSIST");
+        return e && e[0] == '0';
+    }();
+    static const int shared_cap = [] {
+        // OSW_GEMM_GRID=n: at most n workgroups while the CUs are shared
         if (const char* gg = std::getenv("OSW_GEMM_GRID")) return std::max(8, std::min(cus, atoi(gg)) / 8 * 8);
         // one workgroup per CU on 3/4 of the CUs (a multiple of the 8 XCDs): the other quarter
         // never holds an encoder workgroup, so another lane's decoder kernels run there at full
@@ -758,6 +763,7 @@ void launch8p(const GemmArgs& g0, hipStream_t s) {
         // 224: 4864, 160: 4855, measured)
         return std::max(8, cus * 3 / 4 / 8 * 8);
     }();
+    const int grid_cap = per_tile ? 1 << 30 : g.share_cus ? shared_cap : cus;
     gemm8p_kernel<EPI, NOEPI><<<std::min(nwg, std::max(8, grid_cap)), GNT, lds, s>>>(g);
 }
 

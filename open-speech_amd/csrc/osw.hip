@@ -7,6 +7,7 @@
 // serialised by a mutex; independent contexts (one per GPU) run concurrently.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -148,6 +149,9 @@ struct EncBaton {
     std::mutex mu;
     hipEvent_t ev = nullptr;
     bool recorded = false;
+    // calls in flight over the contexts sharing this baton (LaneCall): with more than one,
+    // the encoder GEMMs leave a quarter of the CUs to the other lanes (GemmArgs::share_cus)
+    std::atomic<int> in_call{0};
     ~EncBaton() {
         if (ev) (void)hipEventDestroy(ev);
     }
@@ -168,6 +172,7 @@ struct osw_ctx {
     bool sibling = false;         // weights belong to another context: read-only here
     bool finalized = false;
     std::shared_ptr<EncBaton> baton;  // shared with sibling contexts; null: encoders not serialised
+    bool share_cus = false;           // this call's encoder GEMMs leave CUs to sibling lanes
     // OSW_ENC_PRIO=1: the encoder runs on its own low-priority stream, the decoder on a
     // high-priority `stream` (measured slower: the default is one stream per lane)
     hipStream_t enc_stream = nullptr;
@@ -520,6 +525,18 @@ void setup_workspace(osw_ctx* c) {
     HIPCHK(hipHostMalloc((void**)&c->done_host, sizeof(int), 0));
 }
 
+// A transcription call in flight on a context: counted on the baton its siblings share,
+// and decides whether this call's encoder GEMMs share the CUs (another lane is busy too)
+struct LaneCall {
+    osw_ctx* c;
+    explicit LaneCall(osw_ctx* c_) : c(c_) {
+        c->share_cus = c->baton && c->baton->in_call.fetch_add(1) > 0;
+    }
+    ~LaneCall() {
+        if (c->baton) c->baton->in_call.fetch_sub(1);
+    }
+};
+
 // ------------------------------ GEMM helper ---------------------------------
 GemmArgs gemm_plain(const h16* A, int64_t lda, const h16* Wt, const float* bias, int M, int N, int K, void* C,
                     int64_t ldc, int epi) {
@@ -540,7 +557,9 @@ bool skinny_ok(const GemmArgs& g) {
            (g.epi == EPI_F16 || g.epi == EPI_F16_GELU || g.epi == EPI_F32_RESID || g.epi == EPI_F32);
 }
 
-void run_gemm(osw_ctx* c, const GemmArgs& g, int cls) {
+void run_gemm(osw_ctx* c, const GemmArgs& g0, int cls) {
+    GemmArgs g = g0;
+    g.share_cus = c->share_cus;
     REQUIRE(g.K % 64 == 0, "GEMM K must be a multiple of 64");
     REQUIRE(!g.A_lo || g.epi == EPI_F32, "hi/lo operands feed fp32 outputs only");
     Timed t(c, cls, 2.0 * g.M * g.N * g.K);
@@ -1417,6 +1436,7 @@ int osw_encode_windows(osw_ctx* c, const osw_window* windows, int32_t n) {
         REQUIRE(c && windows, "null argument");
         std::lock_guard<std::mutex> lk(c->mu);
         DeviceScope dev_scope_((c->device));
+        LaneCall call_(c);
         encode(c, windows, n);
         HIPCHK(hipStreamSynchronize(c->stream));
         resolve_events(c);
@@ -1442,6 +1462,7 @@ int osw_decode_windows(osw_ctx* c, int32_t n, const osw_decode_opts* opts, osw_w
         REQUIRE(c, "null ctx");
         std::lock_guard<std::mutex> lk(c->mu);
         DeviceScope dev_scope_((c->device));
+        LaneCall call_(c);
         decode(c, n, opts, res);
         resolve_events(c);
     });
@@ -1454,6 +1475,7 @@ int osw_transcribe_batch(osw_ctx* c, const int16_t* pcm, const int64_t* offsets,
         std::lock_guard<std::mutex> lk(c->mu);
         DeviceScope dev_scope_((c->device));
         REQUIRE(n_clips >= 1 && n_clips <= c->B, "n_clips out of range");
+        LaneCall call_(c);
         log_mel(c, pcm, offsets, n_clips, pcm_on_device, nullptr);
         std::vector<osw_window> wins(n_clips);
         for (int i = 0; i < n_clips; ++i)

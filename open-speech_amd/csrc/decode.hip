@@ -50,44 +50,48 @@ __device__ __forceinline__ h16x8 ld8(const h16* p) {
 // 256 threads.  Scores live in LDS (n_keys <= MAXK).  Loads are issued in groups
 // (8 K pieces = 256 keys, 8 V pieces = 256 keys per lane) before the FMAs that use
 // them, so a 448-key cache costs two HBM round trips per pass (the former 128-key K
-// tiles and one-piece V tail loop cost up to 4 and 8).
+// tiles and one-piece V tail loop cost up to 4 and 8).  Thread t touches the keys
+// (t >> 3) + 32 i (i = 0, 1, ...) in both passes.
 //
 // GATHER (beam search): key p of this row lives in the cache slot of the row that
 // wrote position p of this hypothesis' history: K + soff[p] * slot_stride, where
-// soff[p] = anc[p] - self (staged in LDS; the newest key is always this row's own).
+// soff[p] = anc[p] - self (0 for the newest key, always this row's own), staged in LDS by
+// the caller before its slab reduction's barrier, so the ancestry costs no round trip of
+// its own.
 template <int MAXK, bool GATHER = false, bool NT = !GATHER>
 __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ K, const h16* __restrict__ V,
-                           int n_keys, h16* __restrict__ out, int64_t lo_off, const int* __restrict__ anc = nullptr,
-                           int self = 0, int64_t slot_stride = 0) {
+                           int n_keys, h16* __restrict__ out, int64_t lo_off, const int* soff = nullptr,
+                           int64_t slot_stride = 0) {
     __shared__ float qs[HD];
     __shared__ float sc[MAXK];
     __shared__ float red[8];
     __shared__ f32x4 part[32][17];  // [key group][8 d-chunks x 2 float4]
-    __shared__ int soff[GATHER ? MAXK : 1];
     const int tid = threadIdx.x;
     if (tid < HD) qs[tid] = (float)q16[tid] * 0.125f;  // 1/sqrt(64), exact in fp32
-    if constexpr (GATHER) {
-        for (int p = tid; p < n_keys; p += 256) soff[p] = p + 1 < n_keys ? anc[p] - self : 0;
-    }
     __syncthreads();
     auto krow = [&](const h16* base, int key) -> const h16* {
-        if constexpr (GATHER) return base + (int64_t)soff[key] * slot_stride + (int64_t)key * HD;
+        // (32-bit element offsets: R rows x H x ctx x 64 < 2^31 at <= 1024 windows x 5 beams)
+        if constexpr (GATHER) return base + (soff[key] * (int)slot_stride + key * HD);
         return base + (int64_t)key * HD;
     };
+    constexpr int NBLK = (MAXK + 255) / 256;
     // scores: 8 lanes per key row (lane c holds dims 8c..8c+7), so one wave-instruction
     // reads 8 consecutive K rows = 1 KiB contiguous; 4 such loads in flight per lane;
     // the 8-lane partial dots are combined with 3 xor-shuffles.
-    const int w = tid >> 6, kr = (tid >> 3) & 7, c8 = tid & 7;
+    const int kg = tid >> 3, c8 = tid & 7;
     float q[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) q[i] = qs[8 * c8 + i];
     float mx = -INFINITY;
     // 256 keys (8 loads per lane) per round trip: at most 2 for 448 keys
-    for (int base = 0; base < n_keys; base += 256) {
+#pragma unroll
+    for (int blk = 0; blk < NBLK; ++blk) {
+        const int base = blk * 256;
+        if (base >= n_keys) break;
         h16x8 kv[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int key = min(base + u * 32 + w * 8 + kr, n_keys - 1);
+            const int key = min(base + u * 32 + kg, n_keys - 1);
             kv[u] = ld8<NT>(krow(K, key) + 8 * c8);
         }
 #pragma unroll
@@ -98,7 +102,7 @@ __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ 
             d += xor_lane<1>(d);
             d += xor_lane<2>(d);
             d += xor_lane<4>(d);
-            const int key = base + u * 32 + w * 8 + kr;
+            const int key = base + u * 32 + kg;
             if (key < n_keys) {
                 if (c8 == 0) sc[key] = d;
                 mx = fmaxf(mx, d);
@@ -113,17 +117,19 @@ __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ 
         sum += p;
     }
     sum = block_reduce_sum(sum, red);  // includes __syncthreads: sc visible
-    // PV: thread -> (key group kg = tid>>3, d chunk c = tid&7), keys j = kg + 32 i;
-    // one wave-instruction reads 8 consecutive V rows = 1 KiB contiguous
-    const int kg = tid >> 3, c = tid & 7;
+    // PV: thread -> (key group kg, d chunk c8), keys j = kg + 32 i; one wave-instruction
+    // reads 8 consecutive V rows = 1 KiB contiguous
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     // 8 V pieces per lane per round trip (keys past the end: clamped address, p = 0, so
     // the lane's keys are still accumulated in increasing order with nothing added)
-    for (int j = kg; j < n_keys; j += 32 * 8) {
+#pragma unroll
+    for (int blk = 0; blk < NBLK; ++blk) {
+        const int j = kg + blk * 256;
+        if (j >= n_keys) break;
         h16x8 v[8];
         float p[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = ld8<NT>(krow(V, min(j + 32 * u, n_keys - 1)) + 8 * c);
+        for (int u = 0; u < 8; ++u) v[u] = ld8<NT>(krow(V, min(j + 32 * u, n_keys - 1)) + 8 * c8);
 #pragma unroll
         for (int u = 0; u < 8; ++u) p[u] = j + 32 * u < n_keys ? sc[j + 32 * u] : 0.f;
 #pragma unroll
@@ -131,8 +137,8 @@ __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ 
 #pragma unroll
             for (int e = 0; e < 8; ++e) acc[e] = fmaf(p[u], (float)v[u][e], acc[e]);
     }
-    part[kg][2 * c] = f32x4{acc[0], acc[1], acc[2], acc[3]};
-    part[kg][2 * c + 1] = f32x4{acc[4], acc[5], acc[6], acc[7]};
+    part[kg][2 * c8] = f32x4{acc[0], acc[1], acc[2], acc[3]};
+    part[kg][2 * c8 + 1] = f32x4{acc[4], acc[5], acc[6], acc[7]};
     __syncthreads();
     if (tid < HD) {
         const int cc = tid >> 3, e = tid & 7;
@@ -192,6 +198,9 @@ __device__ __forceinline__ void reduce_qkv(const float* __restrict__ part, int k
 // grid (H, B): q,k,v = Σ split-K partials of the fused qkv projection + bias; k,v
 // appended to the cache at the device-side position; attend over 0..pos.  (Issuing the
 // first K/V batch before the slab reduction left the batch-1 p50 unchanged, measured.)
+// GATHER (beam rows): the row's ancestry is loaded before the slab reduction and staged in
+// LDS behind its barrier, so it lands with the slabs (one round trip) instead of after.
+template <bool GATHER>
 __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restrict__ part, int ks,
                                                             const float* __restrict__ bias, h16* __restrict__ kcache,
                                                             h16* __restrict__ vcache, const int* __restrict__ pos_ptr,
@@ -200,7 +209,7 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
                                                             const SelState* __restrict__ st) {
     __shared__ h16 q16[HD];
     int h, b;
-    if (anc) {
+    if constexpr (GATHER) {
         // beam rows: the `group` hypotheses of one (window, head) run adjacently on one
         // XCD, so the cache rows they share through the ancestry table hit that L2
         const int nwg = gridDim.x, bid = blockIdx.x;
@@ -220,13 +229,28 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
     const int pos = min(*pos_ptr, ctx - 1);  // graph replays may run past max_length on finished windows
     h16* kc = kcache + ((int64_t)b * H + h) * ctx * HD;
     h16* vc = vcache + ((int64_t)b * H + h) * ctx * HD;
+    __shared__ int soff[GATHER ? 512 : 1];
+    int an2[2];  // ancestry of keys tid and tid + 256 (ctx <= 448 < 512), issued before the slab loads
+    if constexpr (GATHER) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int key = threadIdx.x + 256 * i;
+            an2[i] = anc[(int64_t)b * ctx + min(key, ctx - 1)];
+        }
+    }
     const int64_t slab = (int64_t)B * 3 * D, row = (int64_t)b * 3 * D;
     reduce_qkv(part, ks, slab, row, D, h, bias, q16, kc + (int64_t)pos * HD, vc + (int64_t)pos * HD);
+    if constexpr (GATHER) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int key = threadIdx.x + 256 * i;
+            soff[key] = key < pos ? an2[i] - b : 0;  // the newest key (pos) is this row's own
+        }
+    }
     __threadfence_block();
     __syncthreads();
-    if (anc)
-        attend_one<448, true>(q16, kc, vc, pos + 1, out + (int64_t)b * D + h * HD, lo_off, anc + (int64_t)b * ctx, b,
-                              (int64_t)H * ctx * HD);
+    if constexpr (GATHER)
+        attend_one<448, true>(q16, kc, vc, pos + 1, out + (int64_t)b * D + h * HD, lo_off, soff, (int64_t)H * ctx * HD);
     else
         attend_one<448>(q16, kc, vc, pos + 1, out + (int64_t)b * D + h * HD, lo_off);
 }
@@ -734,8 +758,10 @@ static_assert(BEAM_SLICES * 256 * TOPK_VPT >= SEL_SPLIT * 4096, "osw.hip admits 
 // followed by -inf fillers in token order.  Within a row every candidate's score is
 // sum_lp + (x - lse) with one lse per list, monotonic in x, so beam_update ranks these
 // exactly as the former separate top-k pass ranked the scores (score desc, flat index
-// asc); a row whose sum_lp is already -inf (all scores tie at -inf) is the one case
-// where the lists can differ from that pass.
+// asc).  Two known divergences from ranking the rounded scores: a row whose sum_lp is
+// already -inf (all scores tie at -inf), and two different logits whose scores round to
+// the same float at the top-2K cutoff (here the larger logit wins, there the lower flat
+// index); CTranslate2's tie order on such inputs is unpinned (no fixture covers it).
 __device__ __forceinline__ void beam_slice_body(const float* __restrict__ logits, const SelParams& P, int step,
                                                 const unsigned* __restrict__ supmask, const SelState& s,
                                                 SelPart* __restrict__ parts, BeamCand* __restrict__ cand) {
@@ -1140,8 +1166,12 @@ int beam_cand_bytes(int) { return (int)sizeof(BeamCand) * BEAM_SLICES * 2 * MAXK
 void launch_dec_self_attn(const float* part, int ks, const float* bias, h16* kc, h16* vc, const int* pos, int B,
                           int H, int ctx, h16* out, int64_t lo_off, const int* anc, int group, const SelState* st,
                           hipStream_t s) {
-    dec_self_attn_kernel<<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, lo_off, anc,
-                                               anc ? group : 1, st);
+    if (anc)  // ctx <= 448 (osw.hip checks the context at decode)
+        dec_self_attn_kernel<true><<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, lo_off, anc,
+                                                         group, st);
+    else
+        dec_self_attn_kernel<false><<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, lo_off,
+                                                          nullptr, 1, st);
 }
 
 void launch_dec_cross_attn(const float* part, int ks, const float* bias, const h16* xk, const h16* xv, int B, int H,

@@ -1,0 +1,3 @@
+set -e
+cd "$GRAFT_REPO_ROOT"
+BENCH_ARGS="--steps 2 --latency-repeats 0 --beam5 0 --beam5-steps 0 --beam5-latency-repeats 0 --realistic-steps 8 --stream-sessions 0 --no-cpu-baseline" bash tools/gpu_env_ab.sh r03_n "OSW_X=0" "OSW_GEMM_GRID=256" "OSW_GEMM_GRID=224"

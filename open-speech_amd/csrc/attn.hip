@@ -41,7 +41,7 @@ __device__ __forceinline__ h16x4 ds_read_tr(const h16* p) {
 // fp16 P operand); O and l stay relative to the same stale max, so the normalised result
 // is the same softmax, and the 32 O rescale multiplies per tile run only when some lane
 // of the wave raised its max (rare after the first tiles) instead of every tile.
-template <bool LAZY>
+template <bool LAZY, int QT>
 __device__ __forceinline__ void enc_attn_unit(const h16* __restrict__ qkv, h16* __restrict__ out, int T, int H,
                                               int nb, int nqb, int nwg, int bid, h16 (&lds)[2][2][KB * HD]) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -52,16 +52,16 @@ __device__ __forceinline__ void enc_attn_unit(const h16* __restrict__ qkv, h16* 
     const int qq = nwg / 8, rr = nwg % 8, xcd = bid % 8;
     const int lin = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + bid / 8;
     const int qb = lin % nqb, h = (lin / nqb) % H, b = lin / (nqb * H);
-    const int q0 = qb * QB + wave * 32;
+    const int q0 = qb * (64 * QT) + wave * (16 * QT);
     const int64_t head_elems = (int64_t)T * HD;
     const h16* Qh = qkv + (((int64_t)0 * nb + b) * H + h) * head_elems;
     const h16* Kh = qkv + (((int64_t)1 * nb + b) * H + h) * head_elems;
     const h16* Vh = qkv + (((int64_t)2 * nb + b) * H + h) * head_elems;
 
     // Q fragments (B operand): lane: q = q0 + qt*16 + li, d = 32 s + 8 g + j
-    h16x8 qf[2][2];
+    h16x8 qf[QT][2];
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
+    for (int qt = 0; qt < QT; ++qt) {
         const int q = min(q0 + qt * 16 + li, T - 1);
 #pragma unroll
         for (int s = 0; s < 2; ++s) qf[qt][s] = *(const h16x8*)(Qh + (int64_t)q * HD + 32 * s + 8 * g);
@@ -83,11 +83,15 @@ __device__ __forceinline__ void enc_attn_unit(const h16* __restrict__ qkv, h16* 
     };
 
     const float cs = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
-    float mrun[2] = {-INFINITY, -INFINITY};
-    float lrun[2] = {0.f, 0.f};
-    f32x4 o[2][4];
+    float mrun[QT], lrun[QT];
+    f32x4 o[QT][4];
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
+    for (int qt = 0; qt < QT; ++qt) {
+        mrun[qt] = -INFINITY;
+        lrun[qt] = 0.f;
+    }
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o[qt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -107,14 +111,14 @@ __device__ __forceinline__ void enc_attn_unit(const h16* __restrict__ qkv, h16* 
         const int k0 = kt * KB;
 
         // ---- Sᵀ = K Qᵀ : sc[qt][t] holds keys 16t + 4g + i for query li
-        f32x4 sc[2][4];
+        f32x4 sc[QT][4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int row = 16 * t + li;
             const h16x8 k0f = *(const h16x8*)&Kl[row * HD + swz(row, g) * 8];
             const h16x8 k1f = *(const h16x8*)&Kl[row * HD + swz(row, 4 + g) * 8];
 #pragma unroll
-            for (int qt = 0; qt < 2; ++qt) {
+            for (int qt = 0; qt < QT; ++qt) {
                 f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
                 a = __builtin_amdgcn_mfma_f32_16x16x32_f16(k0f, qf[qt][0], a, 0, 0, 0);
                 a = __builtin_amdgcn_mfma_f32_16x16x32_f16(k1f, qf[qt][1], a, 0, 0, 0);
@@ -126,9 +130,9 @@ __device__ __forceinline__ void enc_attn_unit(const h16* __restrict__ qkv, h16* 
         // kept on raw scores and the 1/sqrt(d)*log2(e) scale folds into one FMA per score,
         // keys past T are masked only in the last tile, and exp2 is the bare v_exp_f32
         // (results below 2^-126 flush to 0, irrelevant next to the row maximum's 1).
-        h16x8 pf[2][2];
+        h16x8 pf[QT][2];
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
+        for (int qt = 0; qt < QT; ++qt) {
             float mx = -INFINITY;
 #pragma unroll
             for (int t = 0; t < 4; ++t)
@@ -195,7 +199,7 @@ __device__ __forceinline__ void enc_attn_unit(const h16* __restrict__ qkv, h16* 
                     vf[4 + j] = vb[j];
                 }
 #pragma unroll
-                for (int qt = 0; qt < 2; ++qt)
+                for (int qt = 0; qt < QT; ++qt)
                     o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf[qt][s], o[qt][dt], 0, 0, 0);
             }
         }
@@ -209,7 +213,7 @@ __device__ __forceinline__ void enc_attn_unit(const h16* __restrict__ qkv, h16* 
     // ---- normalise and store: lane holds O[q = li][d = 16 dt + 4 g + i]
     const int D = H * HD;
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
+    for (int qt = 0; qt < QT; ++qt) {
         float l = lrun[qt];
         l += xor_lane<16>(l);
         l += xor_lane<32>(l);
@@ -230,20 +234,30 @@ __device__ __forceinline__ void enc_attn_unit(const h16* __restrict__ qkv, h16* 
 // Persistent over the (q-block, head, window) units when the grid is capped (workgroup b
 // runs units b, b + grid, ...; grid a multiple of 8, so a unit keeps its XCD): like the
 // encoder GEMM, the attention then leaves a quarter of the CUs to another lane's decoder.
-template <bool LAZY>
+// QT: 16-query MFMA tiles per wave (2: 128 queries per workgroup; 1: 64, for one or two
+// windows, where 128-query blocks leave CUs idle: 240 workgroups at one window).  A
+// query's arithmetic does not depend on the queries beside it (the lazy max is per lane;
+// a skipped rescale is a multiply by exactly 1), so both forms give identical results.
+template <bool LAZY, int QT>
 __global__ __launch_bounds__(256, 2) void enc_attn_kernel(const h16* __restrict__ qkv, h16* __restrict__ out,
                                                           int T, int H, int nb, int nqb) {
     __shared__ __attribute__((aligned(16))) h16 lds[2][2][KB * HD];  // [buf][K|V] 32 KiB
     const int nwg = nqb * H * nb;
     for (int vb = blockIdx.x; vb < nwg; vb += gridDim.x) {
-        enc_attn_unit<LAZY>(qkv, out, T, H, nb, nqb, nwg, vb, lds);
+        enc_attn_unit<LAZY, QT>(qkv, out, T, H, nb, nqb, nwg, vb, lds);
         __syncthreads();  // the LDS ring is the next unit's
     }
 }
 }  // namespace
 
 void launch_enc_attn(const h16* qkv, h16* out, int T, int H, int nb, hipStream_t s) {
-    const int nqb = (T + QB - 1) / QB;
+    // 64-query blocks while 128-query ones would give < 2 workgroups per CU (OSW_ATTN_QB: force 64 / 128)
+    static const int qb_env = [] {
+        const char* e = std::getenv("OSW_ATTN_QB");
+        return e ? atoi(e) : 0;
+    }();
+    const bool small = qb_env ? qb_env == 64 : (int64_t)((T + QB - 1) / QB) * H * nb < 512;
+    const int nqb = small ? (T + 63) / 64 : (T + QB - 1) / QB;
     const int nwg = nqb * H * nb;
     static const bool eager = [] {  // OSW_ATTN_LAZY=0: rescale O on every tile (A/B)
         const char* e = std::getenv("OSW_ATTN_LAZY");
@@ -257,8 +271,13 @@ void launch_enc_attn(const h16* qkv, h16* out, int T, int H, int nb, hipStream_t
         return 1 << 30;
     }();
     const int grid = std::min(nwg, cap);
-    if (eager) enc_attn_kernel<false><<<grid, 256, 0, s>>>(qkv, out, T, H, nb, nqb);
-    else enc_attn_kernel<true><<<grid, 256, 0, s>>>(qkv, out, T, H, nb, nqb);
+    if (small) {
+        if (eager) enc_attn_kernel<false, 1><<<grid, 256, 0, s>>>(qkv, out, T, H, nb, nqb);
+        else enc_attn_kernel<true, 1><<<grid, 256, 0, s>>>(qkv, out, T, H, nb, nqb);
+    } else {
+        if (eager) enc_attn_kernel<false, 2><<<grid, 256, 0, s>>>(qkv, out, T, H, nb, nqb);
+        else enc_attn_kernel<true, 2><<<grid, 256, 0, s>>>(qkv, out, T, H, nb, nqb);
+    }
 }
 
 }  // namespace osw

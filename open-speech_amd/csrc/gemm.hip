@@ -60,6 +60,89 @@ __device__ __forceinline__ void store_one(const GemmArgs& g, int m, int n, float
     }
 }
 
+template <int EPI>
+__device__ __forceinline__ float epi_value(const GemmArgs& g, int m, int n, float v) {
+    if (g.bias) v += g.bias[n];
+    if constexpr (EPI == EPI_F16_GELU) v = gelu_erf(v);
+    return v;  // EPI_F32_GELU_POS: GELU + pos applied in the copy-out pass (fewer live registers)
+}
+
+// LDS-staged epilogue of a TM x TM tile held as 2 x 2 waves of (TM/2)^2 (gemm_kernel,
+// gemm64_ring_kernel, gemm128_ring_kernel): bias / GELU applied into an LDS image of the
+// tile (16-B chunks XOR-swizzled by row), then 16-B stores, TM*16 B per wave-instruction,
+// instead of one 2-B / 4-B store per element (fc1's GELU tile at 4 windows: 172 us with
+// per-element stores).  `smem` must hold TM*TM fp32 (every wave past its operand reads).
+template <int EPI, int TM>
+__device__ __forceinline__ void staged_epilogue_sq(const GemmArgs& g, const f32x4 (&acc)[TM / 32][TM / 32], int m0,
+                                                   int n0, int wm, int wn, void* smem, int tid) {
+    static_assert(EPI != EPI_F32, "plain fp32 tiles keep their write-through element stores");
+    constexpr int FT = TM / 32, WT = TM / 2;
+    const int lane = tid & 63;
+    if constexpr (EPI == EPI_F16 || EPI == EPI_F16_GELU || EPI == EPI_HEADS) {
+        h16* T = (h16*)smem;
+        auto at = [](int row, int col) { return row * TM + ((((col >> 3) ^ row) & (TM / 8 - 1)) << 3) + (col & 7); };
+#pragma unroll
+        for (int mi = 0; mi < FT; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < FT; ++ni)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int row = wm * WT + mi * 16 + (lane >> 4) * 4 + i;
+                    const int col = wn * WT + ni * 16 + (lane & 15);
+                    T[at(row, col)] = (h16)epi_value<EPI>(g, m0 + row, min(n0 + col, g.N - 1), acc[mi][ni][i]);
+                }
+        __syncthreads();
+#pragma unroll 4
+        for (int j = 0; j < TM * TM / 8 / NTHR; ++j) {
+            const int id = j * NTHR + tid;
+            const int row = id / (TM / 8), c8 = (id % (TM / 8)) * 8;
+            const int m = m0 + row, n = n0 + c8;
+            if (m >= g.M || n >= g.N) continue;
+            const h16x8 val = *(const h16x8*)&T[at(row, c8)];
+            h16* dst;
+            if constexpr (EPI == EPI_HEADS) {
+                const int D = g.heads_H * 64;
+                const int which = n / D, h = (n % D) >> 6, d = n & 63;
+                const int b = m / g.heads_T, t = m % g.heads_T;
+                dst = (h16*)g.C + ((((int64_t)which * g.heads_nb + b) * g.heads_H + h) * g.heads_T + t) * 64 + d;
+            } else {
+                dst = (h16*)g.C + (m / g.c_grp_rows) * g.c_grp_stride + (int64_t)(m % g.c_grp_rows) * g.ldc + n;
+            }
+            *(h16x8*)dst = val;
+        }
+    } else {
+        float* T = (float*)smem;
+        auto at = [](int row, int col) { return row * TM + ((((col >> 2) ^ row) & (TM / 4 - 1)) << 2) + (col & 3); };
+#pragma unroll
+        for (int mi = 0; mi < FT; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < FT; ++ni)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int row = wm * WT + mi * 16 + (lane >> 4) * 4 + i;
+                    const int col = wn * WT + ni * 16 + (lane & 15);
+                    T[at(row, col)] = epi_value<EPI>(g, m0 + row, min(n0 + col, g.N - 1), acc[mi][ni][i]);
+                }
+        __syncthreads();
+#pragma unroll 4
+        for (int j = 0; j < TM * TM / 4 / NTHR; ++j) {
+            const int id = j * NTHR + tid;
+            const int row = id / (TM / 4), c4 = (id % (TM / 4)) * 4;
+            const int m = m0 + row, n = n0 + c4;
+            if (m >= g.M || n >= g.N) continue;
+            f32x4 val = *(const f32x4*)&T[at(row, c4)];
+            float* dst = (float*)g.C + (m / g.c_grp_rows) * g.c_grp_stride + (int64_t)(m % g.c_grp_rows) * g.ldc + n;
+            if constexpr (EPI == EPI_F32_RESID) val += *(const f32x4*)dst;
+            if constexpr (EPI == EPI_F32_GELU_POS) {
+                const f32x4 pv = *(const f32x4*)&g.pos[(int64_t)(m % g.c_grp_rows) * g.N + n];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) val[e] = gelu_erf(val[e]) + pv[e];
+            }
+            *(f32x4*)dst = val;
+        }
+    }
+}
+
 // TM = 128 (the default) or 64: the 64x64 tile for small M (the encoder of one or a few
 // windows: 1500 rows give a 128-tile N = 1280 GEMM only 120 workgroups for 256 CUs).
 // Every output element is the same MFMA chain over K in the same order at either tile
@@ -155,6 +238,10 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
             }
         return;
     }
+    if constexpr (EPI != EPI_F32) {  // 16-B chunk stores through an LDS image (loop drained: LDS free)
+        staged_epilogue_sq<EPI, TM>(g, acc, m0, n0, wm, wn, &lds[0][0][0], threadIdx.x);
+        return;
+    }
 #pragma unroll
     for (int mi = 0; mi < FT; ++mi)
 #pragma unroll
@@ -200,12 +287,6 @@ constexpr int EPI_LDS = 256 * 256 * 2;  // 131072 B = 128 rows x 256 fp32
 __device__ __forceinline__ int ep16(int row, int col) { return row * 256 + ((((col >> 3) ^ row) & 31) << 3) + (col & 7); }
 __device__ __forceinline__ int ep32(int row, int col) { return row * 256 + ((((col >> 2) ^ row) & 63) << 2) + (col & 3); }
 
-template <int EPI>
-__device__ __forceinline__ float epi_value(const GemmArgs& g, int m, int n, float v) {
-    if (g.bias) v += g.bias[n];
-    if constexpr (EPI == EPI_F16_GELU) v = gelu_erf(v);
-    return v;  // EPI_F32_GELU_POS: GELU + pos applied in the copy-out pass (fewer live registers)
-}
 
 // IL = false: wave (wm, wn) owns rows wm*128 + [0,128) and cols wn*64 + [0,64).
 // IL = true (8-phase kernel): rows {0,128} + wm*64 + [0,64), cols {0,128} + wn*32 + [0,32).
@@ -768,18 +849,139 @@ void launch8p(const GemmArgs& g0, hipStream_t s) {
 }
 
 
-// ---------------------------------------------------------------------------
-// Skinny GEMM for the decoder (M <= 64 rows = windows in the batch): weight-
-// bandwidth bound, so the grid is split over N (64 columns per workgroup, 16 per
-// wave) AND over K (ksplit partial slabs, reduced deterministically by a second
-// kernel that also applies the epilogue).  Operands go straight to VGPRs
-// (no LDS: nothing is shared between waves but the tiny, L2-resident A).
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
     // s_waitcnt vmcnt(N) with expcnt/lgkmcnt left at their maxima (gfx9 encoding)
     static_assert(N < 64, "vmcnt range");
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
+
+// ---------------------------------------------------------------------------
+// Mid-M encoder GEMM (one to a few windows: 1500-12000 rows): 128x128x64 tiles, 4 waves
+// of 64x64, and a 4-slot LDS ring (128 KiB, one workgroup per CU) that keeps three K
+// tiles in flight.  The double-buffered 128 tile waited one load round trip per K step
+// (fc1 at 4 windows: ~2.3 us per 64-deep step, 18 % of the CU's MFMA rate); the 64 tile
+// hides the latency but moves 2x the operand bytes per flop.  Counted vmcnt + raw
+// s_barrier as in gemm64_ring_kernel.  Tiles are dealt XCD-contiguously, each XCD's run
+// walking down M for one column block (its weight panel stays L2-hot).  The output
+// leaves through an LDS image of the tile (16-B stores, 2 KiB per wave-instruction).
+// Every output element is the same MFMA chain over K in the same order as in the other
+// tile sizes: identical results.
+constexpr int R128_NS = 4, R128_SLOT = 2 * 128 * BK;                   // halfs per ring slot
+constexpr int R128_LDS = R128_NS * R128_SLOT * 2;                      // 131072 B
+
+template <int EPI>
+__global__ __launch_bounds__(NTHR, 1) void gemm128_ring_kernel(GemmArgs g) {
+    constexpr int TM = 128, PW = 4, FT = 4, WT = 64;
+    extern __shared__ __attribute__((aligned(16))) h16 smem[];  // [NS][A|W][128*64]
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int ntm = (g.M + TM - 1) / TM, ntn = (g.N + TM - 1) / TM, nwg = ntm * ntn;
+    const int bid = blockIdx.x, q = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+    const int v = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + bid / 8;
+    const int m0 = (v % ntm) * TM, n0 = (v / ntm) * TM;
+    const h16* asrc[PW];
+    const h16* wsrc[PW];
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+        const int r = (i * 4 + wave) * 8 + (lane >> 3);
+        const int c = swz(r, lane & 7);
+        asrc[i] = grp_row(g.A, min(m0 + r, g.M - 1), g.a_grp_rows, g.a_grp_stride, g.lda) + c * 8;
+        wsrc[i] = g.W + (int64_t)min(n0 + r, g.N - 1) * g.ldw + c * 8;
+    }
+    auto stage = [&](int slot, int k0) {
+        h16* base = smem + slot * R128_SLOT;
+#pragma unroll
+        for (int i = 0; i < PW; ++i) {
+            __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + k0), (OSW_LDS void*)(base + (i * 4 + wave) * 8 * BK),
+                                             16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + k0),
+                                             (OSW_LDS void*)(base + TM * BK + (i * 4 + wave) * 8 * BK), 16, 0, 0);
+        }
+    };
+    const int wm = wave >> 1, wn = wave & 1;
+    f32x4 acc[FT][FT];
+#pragma unroll
+    for (int i = 0; i < FT; ++i)
+#pragma unroll
+        for (int j = 0; j < FT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nk = g.K / BK;
+#pragma unroll
+    for (int s = 0; s < R128_NS - 1; ++s)
+        if (s < nk) stage(s, s * BK);
+    for (int kt = 0; kt < nk; ++kt) {
+        // tile kt has landed once at most min(NS-2, nk-1-kt) younger tiles are in flight
+        const int ahead = min(R128_NS - 2, nk - 1 - kt);
+        if (ahead >= 2) wait_vmcnt<2 * 2 * PW>();
+        else if (ahead == 1) wait_vmcnt<2 * PW>();
+        else wait_vmcnt<0>();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave's pieces of tile kt landed; slot (kt-1) % NS is free
+        asm volatile("" ::: "memory");
+        if (kt + R128_NS - 1 < nk) stage((kt + R128_NS - 1) % R128_NS, (kt + R128_NS - 1) * BK);
+        const h16* la = smem + (kt % R128_NS) * R128_SLOT;
+        const h16* lw = la + TM * BK;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int c = ks * 4 + (lane >> 4);
+            h16x8 a[FT], b[FT];
+#pragma unroll
+            for (int mi = 0; mi < FT; ++mi) {
+                const int row = wm * WT + mi * 16 + (lane & 15);
+                a[mi] = *(const h16x8*)&la[row * BK + swz(row, c) * 8];
+            }
+#pragma unroll
+            for (int ni = 0; ni < FT; ++ni) {
+                const int row = wn * WT + ni * 16 + (lane & 15);
+                b[ni] = *(const h16x8*)&lw[row * BK + swz(row, c) * 8];
+            }
+#pragma unroll
+            for (int mi = 0; mi < FT; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < FT; ++ni)
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+        }
+    }
+    // epilogue through an LDS image of the tile (the ring is free once every wave is past
+    // its last fragment read)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    if constexpr (EPI != EPI_F32) {
+        staged_epilogue_sq<EPI, TM>(g, acc, m0, n0, wm, wn, smem, threadIdx.x);
+    } else {  // (debug entry only) plain fp32 tile
+#pragma unroll
+        for (int mi = 0; mi < FT; ++mi)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int m = m0 + wm * WT + mi * 16 + (lane >> 4) * 4 + i;
+                if (m >= g.M) continue;
+#pragma unroll
+                for (int ni = 0; ni < FT; ++ni) {
+                    const int n = n0 + wn * WT + ni * 16 + (lane & 15);
+                    if (n < g.N) ((float*)g.C)[(m / g.c_grp_rows) * g.c_grp_stride + (int64_t)(m % g.c_grp_rows) * g.ldc + n] =
+                        g.bias ? acc[mi][ni][i] + g.bias[n] : acc[mi][ni][i];
+                }
+            }
+    }
+}
+
+template <int EPI>
+void launch_ring128(const GemmArgs& g, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)gemm128_ring_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  R128_LDS);
+        attr = true;
+    }
+    const int nwg = ((g.N + 127) / 128) * ((g.M + 127) / 128);
+    gemm128_ring_kernel<EPI><<<nwg, NTHR, R128_LDS, s>>>(g);
+}
+
+// ---------------------------------------------------------------------------
+// Skinny GEMM for the decoder (M <= 64 rows = windows in the batch): weight-
+// bandwidth bound, so the grid is split over N (64 columns per workgroup, 16 per
+// wave) AND over K (ksplit partial slabs, reduced deterministically by a second
+// kernel that also applies the epilogue).  Operands go straight to VGPRs
+// (no LDS: nothing is shared between waves but the tiny, L2-resident A).
 
 // Small-M encoder GEMM (one or a few windows): 64x64 tiles (4 waves of 32x32) with a
 // 4-slot LDS ring that keeps three K tiles in flight.  A 64-tile K step is only 8 MFMAs
@@ -855,6 +1057,12 @@ __global__ __launch_bounds__(NTHR, 2) void gemm64_ring_kernel(GemmArgs g) {
                 for (int ni = 0; ni < FT; ++ni)
                     acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
         }
+    }
+    if constexpr (EPI != EPI_F32) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();  // every wave past its last fragment read: the ring holds the image
+        staged_epilogue_sq<EPI, TM>(g, acc, m0, n0, wm, wn, &lds[0][0][0], threadIdx.x);
+        return;
     }
 #pragma unroll
     for (int mi = 0; mi < FT; ++mi)
@@ -1545,9 +1753,17 @@ void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s) {
         launch_wide(g, 1, s);
         return;
     }
-    // big tile when it still yields >= 2 waves of workgroups over 256 CUs
+    // Tile choice by tile count (every tile size gives identical results; measured on the
+    // encoder shapes at 1-8 windows, tools/small_gemm_bench.py, profiles/r03_q_small_gemm.jsonl):
+    // the 8-phase 256 tile from 180 tiles on (~0.7 of the CUs: at 2 windows fc1 47 vs 70 us
+    // on the 128 tile, the cross-K/V GEMM at one window 48 vs 70 us), below that the 128
+    // tile from 360 tiles, the 128 ring from 192, the 64 ring under it.
+    static const int p8_min = [] {
+        const char* e = getenv("OSW_8P_MIN");
+        return e ? atoi(e) : 180;
+    }();
     const int64_t big_tiles = (int64_t)((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
-    const bool big = !g.A_lo && (variant == 2 || (variant == 0 && big_tiles >= 512 && g.N % 8 == 0 &&
+    const bool big = !g.A_lo && (variant == 2 || (variant == 0 && big_tiles >= p8_min && g.N % 8 == 0 &&
                                                    !getenv("OSW_GEMM128")));
 
     static const bool two_phase = getenv("OSW_GEMM_2PHASE") != nullptr;  // A/B switch for the 8-phase schedule
@@ -1583,16 +1799,38 @@ void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s) {
             default: launch256<EPI_HEADS>(g, s); return;
         }
     }
+    const int64_t tiles128 = (int64_t)((g.N + BN - 1) / BN) * ((g.M + BM - 1) / BM);
+    // 128 ring for [r128_min, db128_min) tiles (OSW_RING128_MIN / OSW_DB128_MIN: A/B switches)
+    static const int r128_min = [] {
+        const char* e = getenv("OSW_RING128_MIN");
+        return e ? atoi(e) : 192;
+    }();
+    static const int db128_min = [] {
+        const char* e = getenv("OSW_DB128_MIN");
+        return e ? atoi(e) : 360;
+    }();
+    // (16-B copy-out chunks: N and the row strides a multiple of 8)
+    const bool r128_ok = g.N % 8 == 0 && (g.epi == EPI_HEADS || g.ldc % 8 == 0) && g.c_grp_stride % 8 == 0;
+    if (r128_ok && (variant == 11 || (variant == 0 && g.kc == 0 && !g.A_lo && g.epi != EPI_F32 &&
+                                      tiles128 >= r128_min && tiles128 < db128_min))) {
+        switch (g.epi) {
+            case EPI_F16: launch_ring128<EPI_F16>(g, s); return;
+            case EPI_F16_GELU: launch_ring128<EPI_F16_GELU>(g, s); return;
+            case EPI_F32_RESID: launch_ring128<EPI_F32_RESID>(g, s); return;
+            case EPI_F32_GELU_POS: launch_ring128<EPI_F32_GELU_POS>(g, s); return;
+            case EPI_F32: launch_ring128<EPI_F32>(g, s); return;
+            default: launch_ring128<EPI_HEADS>(g, s); return;
+        }
+    }
     // fewer than 2 workgroups per CU on the 128 tile (small M: one or a few encoder
     // windows): the 64 tile, 4x the workgroups, identical results
     static const bool no_small = getenv("OSW_NO_TILE64") != nullptr;  // A/B switch
-    const int64_t tiles128 = (int64_t)((g.N + BN - 1) / BN) * ((g.M + BM - 1) / BM);
-    if (variant == 6 || variant == 7 || (!no_small && variant == 0 && g.kc == 0 && tiles128 < 512)) {
+    if (variant == 6 || variant == 7 || (!no_small && variant == 0 && g.kc == 0 && tiles128 < r128_min)) {
         dim3 grid((g.N + 63) / 64, (g.M + 63) / 64);
-        // the 4-slot ring (64 KB, 2 workgroups per CU) for long K (fc2: 70 -> 45 us at one
-        // window); at K = 1280 the double-buffered kernel's occupancy wins (qkv 43 vs 50 us)
+        // the 4-slot ring (64 KB, 2 workgroups per CU): fc2 at one window 70 -> 39 us, the
+        // out-projection 16 -> 14.5 us
         static const bool no_ring = getenv("OSW_NO_RING64") != nullptr;  // A/B switch
-        if (variant == 6 || (variant == 0 && !no_ring && g.K > 2048)) {
+        if (variant == 6 || (variant == 0 && !no_ring)) {
             switch (g.epi) {
                 case EPI_F16: gemm64_ring_kernel<EPI_F16><<<grid, NTHR, 0, s>>>(g); break;
                 case EPI_F16_GELU: gemm64_ring_kernel<EPI_F16_GELU><<<grid, NTHR, 0, s>>>(g); break;

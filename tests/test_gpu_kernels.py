@@ -25,7 +25,8 @@ def eng():
     (3, 64, 51866, 1280), (3, 16, 384, 1536), (3, 3, 700, 128), (3, 50, 40000, 640),
     (5, 64, 51866, 1280), (5, 1, 51866, 1280), (5, 37, 20000, 384), (5, 64, 300, 64), (5, 5, 1000, 128),
     (6, 1500, 1280, 1280), (6, 300, 200, 128), (6, 1500, 5120, 1280), (6, 1500, 1280, 5120),
-    (7, 1500, 1280, 1280), (7, 300, 200, 128)])
+    (7, 1500, 1280, 1280), (7, 300, 200, 128), (11, 1500, 1280, 1280), (11, 300, 200, 128),
+    (11, 1500, 5120, 1280), (11, 1500, 1280, 5120), (11, 6000, 3840, 1280), (11, 2999, 776, 192)])
 def test_gemm_variants(eng, variant, M, N, K):
     rng = np.random.default_rng(M * 7 + N)
     A = rng.uniform(-1, 1, (M, K)).astype(np.float16)
@@ -39,7 +40,7 @@ def test_gemm_variants(eng, variant, M, N, K):
 @pytest.mark.parametrize("M,N,K", [(1500, 1280, 1280), (3000, 2304, 1280), (1500, 1280, 5120), (777, 264, 128)])
 def test_tile_sizes_bit_identical(eng, M, N, K):
     """The encoder GEMM picks its tile by M (64 for one or a few windows, with or without
-    the deep LDS ring, 128, or the
+    the deep LDS ring, 128 with or without the 4-slot ring, or the
     8-phase 256 at large M): every output element is the same MFMA chain over K in the
     same order, so a window's encoder output does not depend on its batch."""
     rng = np.random.default_rng(M + N + K)
@@ -49,6 +50,8 @@ def test_tile_sizes_bit_identical(eng, M, N, K):
     c6, _ = eng.debug_gemm(A, W, 6)
     c7, _ = eng.debug_gemm(A, W, 7)
     c4, _ = eng.debug_gemm(A, W, 4)
+    c11, _ = eng.debug_gemm(A, W, 11)
+    assert np.array_equal(c1, c11)
     assert np.array_equal(c1, c6)
     assert np.array_equal(c1, c7)
     assert np.array_equal(c1, c4)

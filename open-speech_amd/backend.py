@@ -113,6 +113,7 @@ class HipWhisperBackend:
             src = model_store.resolve(model_id, self._settings.get("stt_model_dir", None))
             max_batch = int(os.environ.get("STT_HIP_MAX_BATCH", "16"))
             wait_ms = float(os.environ.get("STT_HIP_BATCH_WAIT_MS", "5"))
+            gap_ms = float(os.environ.get("STT_HIP_BATCH_GAP_MS", "1"))
             factory = self._engine_factory or _default_engine_factory
             engines = []
             try:
@@ -134,7 +135,7 @@ class HipWhisperBackend:
                     e.close()
                 raise
             tok = WhisperTokenizer(src.dims.n_vocab, src.tokenizer_json)
-            runner = BatchRunner(engines, tok, max_wait_ms=wait_ms)
+            runner = BatchRunner(engines, tok, max_wait_ms=wait_ms, gap_ms=gap_ms)
             self._models[model_id] = _Model(src, runner, tok, engines)
             now = time.time()
             self._loaded_at[model_id] = now

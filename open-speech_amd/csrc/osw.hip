@@ -947,6 +947,12 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
             c->dgraph = nullptr;
             HIPCHK(hipStreamSynchronize(c->stream));
             hipGraph_t gr = nullptr;
+            // A sibling lane's encoder waits on the baton event, which this lane may have
+            // recorded on this stream: HIP refuses that wait while this stream captures
+            // ("dependency created on uncaptured work in another stream"), so no sibling
+            // enqueues an encoder (which holds the baton's mutex) during a capture.
+            std::unique_lock<std::mutex> no_encoder;
+            if (c->baton) no_encoder = std::unique_lock<std::mutex>(c->baton->mu);
             c->capturing = true;
             try {
                 HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));

@@ -5,7 +5,7 @@ The reference calls ``transcribe`` concurrently from the default executor (REST,
 4-thread Realtime pool (``src/realtime/server.py:33-35``) and Wyoming.  Each call
 here becomes a request on a queue; one worker thread per GPU drains up to
 ``max_batch`` requests (waiting at most ``max_wait_ms`` for company once the first
-arrives), runs them as one batched seek loop on its engine, and completes each
+arrives, and at most ``gap_ms`` after the latest arrival), runs them as one batched seek loop on its engine, and completes each
 caller's future.  Requests are routed to the worker with the shortest queue
 (multi-GPU serving: independent clips, no collective).  A worker whose GPU fails
 marks every worker of that GPU (its sibling lanes) dead and re-queues the requests
@@ -49,9 +49,17 @@ class _Worker(threading.Thread):
             if first is None:
                 return
             batch = [first]
-            deadline = time.monotonic() + self.pool.max_wait_ms / 1000.0
+            now = time.monotonic()
+            deadline = now + self.pool.max_wait_ms / 1000.0
+            gap = self.pool.gap_ms / 1000.0 if self.pool.gap_ms is not None else None
+            last = now
             while len(batch) < self.engine.max_batch:
-                left = deadline - time.monotonic()
+                # wait for company until max_wait after the first request, or gap after the
+                # latest one (callers released together by the previous batch arrive within
+                # a fraction of a millisecond; waiting the whole max_wait for a 5th that the
+                # 4-thread streaming pool can never send cost ~4 ms per call)
+                end = deadline if gap is None else min(deadline, last + gap)
+                left = end - time.monotonic()
                 try:
                     nxt = self.q.get(timeout=max(0.0, left)) if left > 0 else self.q.get_nowait()
                 except queue.Empty:
@@ -60,6 +68,7 @@ class _Worker(threading.Thread):
                     self.q.put(None)
                     break
                 batch.append(nxt)
+                last = time.monotonic()
             self.inflight = len(batch)
             try:
                 self._run_batch(batch)
@@ -89,9 +98,11 @@ class _Worker(threading.Thread):
 
 
 class BatchRunner:
-    def __init__(self, engines: list, tokenizer: WhisperTokenizer, max_wait_ms: float = 5.0):
+    def __init__(self, engines: list, tokenizer: WhisperTokenizer, max_wait_ms: float = 5.0,
+                 gap_ms: float | None = None):
         self.tokenizer = tokenizer
         self.max_wait_ms = max_wait_ms
+        self.gap_ms = gap_ms
         self._sup_cache: dict = {}
         self._lock = threading.Lock()
         self.workers = [_Worker(self, e, i) for i, e in enumerate(engines)]

@@ -367,3 +367,39 @@ def test_cache_listing_with_stt_model_dir(tmp_path, monkeypatch):
     monkeypatch.setenv("HF_HUB_CACHE", str(tmp_path))
     b2 = make_backend()
     assert {m["model"] for m in b2.list_cached_models()} == {"Systran/faster-whisper-base"}
+
+
+def test_batcher_gap_ends_collection_early():
+    """The batcher stops waiting gap_ms after the latest arrival instead of max_wait_ms
+    after the first: requests queued together still form one batch, a lone request is
+    not held for the whole max_wait."""
+    import time as _t
+    from concurrent.futures import Future
+    from open_speech_amd.runner import BatchRunner, _Req
+    from open_speech_amd.segments import TranscribeOptions
+    from open_speech_amd.tokenizer import WhisperTokenizer
+
+    class Eng(FakeEngine):
+        def __init__(self):
+            super().__init__(D.MICRO_TEST, 0, 8,
+                             lambda w, i, p, l: WindowOutput([TB, 1000, TB + 50], -1.0, 0.01, ST.first_lang))
+            self.batches = []
+
+        def decode(self, n, cfg, prefix=None, dump_steps=0, languages=None):
+            self.batches.append(n)
+            return super().decode(n, cfg, prefix, dump_steps, languages)
+
+    e = Eng()
+    runner = BatchRunner([e], WhisperTokenizer(51866), max_wait_ms=2000, gap_ms=50)
+    try:
+        reqs = [_Req(synth.chirp_clip(i, 3.0), TranscribeOptions(beam_size=1, language="en"), Future())
+                for i in range(3)]
+        t0 = _t.monotonic()
+        for r in reqs:
+            runner.workers[0].q.put(r)
+        for r in reqs:
+            r.fut.result(timeout=30)
+        assert e.batches and set(e.batches) == {3}   # every seek-loop call carries all three
+        assert _t.monotonic() - t0 < 1.5   # not the 2 s max_wait
+    finally:
+        runner.close()

@@ -434,3 +434,51 @@ def test_token_budget_and_finished_rows(tiny_engine):
             assert cut[i].tokens == free[i].tokens[:b], i
         else:
             assert cut[i].tokens == free[i].tokens and cut[i].sum_logprob == free[i].sum_logprob, i
+
+
+def test_sibling_encodes_while_lane_captures_graphs(tiny_engine):
+    """One lane captures new decode graphs (a new key per call: max_length varies) while a
+    sibling lane keeps encoding, whose encoder waits on the shared baton event.  HIP refuses
+    a wait on an event recorded by a stream that is capturing at that moment ("dependency
+    created on uncaptured work in another stream"), which failed config-5 calls spread over
+    the lanes (r03_s); captures now exclude sibling encoder enqueues.  Every call succeeds
+    and gives the lone run's tokens."""
+    import threading
+    d, eng, w = tiny_engine
+    sib = eng.sibling(max_batch=2)
+    try:
+        sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+        clips = [synth.chirp_clip(41, 30.0), synth.chirp_clip(42, 9.0)]
+        cfgs = [DecodeConfig(suppress_tokens=sup, max_length=L, beam_size=bs) for L in (40, 48, 56, 64, 72)
+                for bs in (1, 5)]
+        ref = [eng.transcribe_batch(clips, c) for c in cfgs[:2]]
+        errs, got = [], []
+        stop = threading.Event()
+
+        def capture_lane():
+            try:
+                for c in cfgs:       # every config is a new graph key on this lane
+                    got.append(eng.transcribe_batch(clips, c))
+            except Exception as e:   # noqa: BLE001
+                errs.append(e)
+            finally:
+                stop.set()
+
+        def encode_lane():
+            try:
+                sib.log_mel(clips)
+                while not stop.is_set():
+                    sib.encode([(0, 0, 3000), (1, 0, 899)])
+            except Exception as e:   # noqa: BLE001
+                errs.append(e)
+
+        th = [threading.Thread(target=capture_lane), threading.Thread(target=encode_lane)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        assert not errs, errs
+        for outs, r in zip(got[:2], ref):
+            assert [o.tokens for o in outs] == [o.tokens for o in r]
+    finally:
+        sib.close()

@@ -19,6 +19,7 @@ from open_speech_amd.audio import pcm_to_wav  # noqa: E402
 from open_speech_amd.backend import HipWhisperBackend  # noqa: E402
 
 R = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+SEQ_ONLY = "--sequential-only" in sys.argv
 MID = "random:large-v3-turbo"
 os.environ.setdefault("STT_HIP_TOKENS_PER_SEC", "4")
 be = HipWhisperBackend()
@@ -36,6 +37,9 @@ for s, w in wavs.items():
     call(w)
     lat = [call(w) for _ in range(R)]
     print(f"sequential {s:.0f} s: p50 {np.median(lat):.1f} ms min {min(lat):.1f}")
+if SEQ_ONLY:
+    be.unload_model(MID)
+    sys.exit(0)
 lat = []
 lock = threading.Lock()
 

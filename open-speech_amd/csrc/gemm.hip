@@ -1127,12 +1127,29 @@ __device__ __forceinline__ SelPart sel_block_merge(SelPart r, SelPart* wp) {
 // into the slice statistics exactly as select_partial_body does; the workgroup's record
 // goes to parts[blockIdx.x] and the last workgroup to arrive merges all records in
 // workgroup order, finalises the row and advances the step counter.
-__device__ __forceinline__ void fused_select_row(float x, int col, bool valid, const SelFuse& F) {
+// The step counter, the row's state and the lane's suppress-mask word are loaded when the
+// workgroup starts (SelPre), in the shadow of the weight stream, not after the GEMM: two
+// dependent round trips fewer at every workgroup's end (the last arriver writes them only
+// after every workgroup has taken its ticket, i.e. after every workgroup loaded them).
+struct SelPre {
+    int step;
+    SelState s;
+    unsigned supw;
+};
+__device__ __forceinline__ SelPre sel_preload(const SelFuse& F, int col) {
+    SelPre q;
+    q.step = *F.pos;
+    q.s = F.st[0];
+    q.supw = F.supmask[min(col, F.P.V - 1) >> 5];
+    return q;
+}
+
+__device__ __forceinline__ void fused_select_row(float x, int col, bool valid, const SelFuse& F, const SelPre& pre) {
     __shared__ SelPart wp[4];
     __shared__ int last;
     const SelParams& P = F.P;
-    const int step = *F.pos;
-    const SelState s = F.st[0];
+    const int step = pre.step;
+    const SelState s = pre.s;
     const int mode = sel_mode(P, step, s);
     const SelPart id{-INFINITY, 0.f, -INFINITY, 0.f, -INFINITY, -INFINITY, -INFINITY, 0x7fffffff, 0x7fffffff,
                      0x7fffffff};
@@ -1143,7 +1160,7 @@ __device__ __forceinline__ void fused_select_row(float x, int col, bool valid, c
         if (mode == SEL_SOT) {
             lse_add(r.m_all, r.s_all, x);
             if (v >= P.first_lang && v < P.first_lang + P.n_langs) a_text = ArgMax{x, v};
-        } else if (!tok_masked_w(P, row_rules(P, s), F.supmask[v >> 5], v)) {
+        } else if (!tok_masked_w(P, row_rules(P, s), pre.supw, v)) {
             lse_add(r.m_all, r.s_all, x);
             a_all = ArgMax{x, v};
             if (v >= P.tb) {
@@ -1246,6 +1263,8 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
     const int k0 = ks * kc;
     const int n = min(nb + (lane & 15), g.N - 1);
     const h16* wrow = g.W + (int64_t)n * g.ldw + k0 + 8 * (lane >> 4);
+    SelPre sel_pre{};
+    if constexpr (SEL) sel_pre = sel_preload(pa.sel, nb + (lane & 15));
     const int nsteps = kc / 32;  // multiple of 4
     const int nch = (nsteps + CK - 1) / CK;
 
@@ -1415,7 +1434,7 @@ store:
         static_assert(MT == 1 && DIRECT, "the fused selection serves the batch-1 logits GEMM");
         const bool valid = gq == 0 && col < g.N;
         if (valid) __hip_atomic_store((float*)g.C + col, acc[0][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        fused_select_row(acc[0][0], col, valid, pa.sel);
+        fused_select_row(acc[0][0], col, valid, pa.sel, sel_pre);
         return;
     }
     if (col >= g.N) return;

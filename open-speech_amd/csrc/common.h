@@ -131,6 +131,10 @@ struct GemmArgs {
     // 8-phase persistent GEMM: 1 = leave a quarter of the CUs to other lanes' kernels (set
     // while sibling contexts have calls in flight), 0 = one workgroup on every CU
     int share_cus;
+    // skinny kernel: W's fragment-major copy, [ceil(N/16)][K/32][64 lanes][8] (the 16 x 32
+    // MFMA B fragment of one k32 step is 1 KB contiguous, so a wave's weight load is one
+    // coalesced 1-KB piece instead of 16 rows x 64 B; launch_frag_pack), or nullptr
+    const h16* Wf;
 };
 
 // fp32 -> (hi, lo) fp16 pair: hi = fp16(v), lo = fp16(v - hi)
@@ -142,6 +146,8 @@ __device__ __forceinline__ void split_h16(float v, h16* hi, h16* lo, int64_t i) 
 
 // launchers (defined in the .hip files)
 void launch_gemm(const GemmArgs& g, hipStream_t s);
+// W[N][ldw] (K columns used) -> its fragment-major copy Wf (GemmArgs::Wf), zero past N
+void launch_frag_pack(const h16* W, int64_t ldw, int N, int K, h16* Wf, hipStream_t s);
 void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s);  // 0 auto, 1 128-tile, 2 256-tile,
                                                                           // 4 8-phase 256, 5 wide, 6 64-tile ring, 7 64-tile;
                                                                           // debug: 8 8-phase fp16 out, 9 no epilogue, 10 GELU

@@ -1261,8 +1261,20 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
     const int ks = by;
     const int mb = bz * ROWS;  // row group (partial mode, M > 64: beam rows)
     const int k0 = ks * kc;
-    const int n = min(nb + (lane & 15), g.N - 1);
-    const h16* wrow = g.W + (int64_t)n * g.ldw + k0 + 8 * (lane >> 4);
+    // this lane's weights: column nb + (lane & 15), k = k0 + 8 (lane >> 4) + 32 st
+    const h16* wrow;
+    int wss;  // h16 per k32 step
+    if (g.Wf) {
+        // fragment-major copy: the wave's 16 x 32 fragment of step st is 1 KB contiguous
+        // (a block past the padded N repeats the last one; its columns are discarded)
+        const int blk = min(nb, ((g.N + 15) & ~15) - 16) >> 4;
+        wrow = g.Wf + ((int64_t)blk * (g.K >> 5) + (k0 >> 5)) * 512 + lane * 8;
+        wss = 512;
+    } else {
+        const int n = min(nb + (lane & 15), g.N - 1);
+        wrow = g.W + (int64_t)n * g.ldw + k0 + 8 * (lane >> 4);
+        wss = 32;
+    }
     SelPre sel_pre{};
     if constexpr (SEL) sel_pre = sel_preload(pa.sel, nb + (lane & 15));
     const int nsteps = kc / 32;  // multiple of 4
@@ -1299,7 +1311,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
             const int st = min(c * CK + u, nsteps - 1);
             // (nt loads measured 8.1 vs 7.2 us on the projections: their weights are re-read
             // every step; nt on the logits stream alone left the batch-1 p50 unchanged)
-            wf[u] = *(const h16x8*)(wrow + 32 * st);
+            wf[u] = *(const h16x8*)(wrow + (int64_t)wss * st);
         }
     };
     f32x4 acc[MT];
@@ -1345,7 +1357,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
             constexpr int AL = NIMG * APIECES;   // LDS-DMA loads per lane per chunk
             h16x8 w[WALL];
 #pragma unroll
-            for (int u = 0; u < WALL; ++u) w[u] = *(const h16x8*)(wrow + 32 * min(u, nsteps - 1));
+            for (int u = 0; u < WALL; ++u) w[u] = *(const h16x8*)(wrow + (int64_t)wss * min(u, nsteps - 1));
             stageA(0, 0);
             if (nch > 1) stageA(1, 1);
 #pragma unroll
@@ -1723,6 +1735,28 @@ int launch_gemm_skinny_pro(const GemmArgs& g, int pro, const ProArgs& pa, bool d
         else gemm_skinny_kernel<1, false, EPI_F32, true, PRO_GELU><<<grid, 256, 0, s>>>(g, kc, part, pa);
     }
     return ks;
+}
+
+// one thread per 16-B piece of Wf: piece p = (blk * K/32 + st) * 64 + lane holds
+// W[blk*16 + (lane & 15)][st*32 + 8 (lane >> 4) .. +8]
+__global__ __launch_bounds__(256) void frag_pack_kernel(const h16* __restrict__ W, int64_t ldw, int N, int K,
+                                                        h16* __restrict__ Wf, int64_t pieces) {
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= pieces) return;
+    const int lane = (int)(p & 63);
+    const int64_t t = p >> 6;
+    const int ks = K >> 5;
+    const int st = (int)(t % ks);
+    const int n = (int)(t / ks) * 16 + (lane & 15);
+    const int k = st * 32 + 8 * (lane >> 4);
+    h16x8 v = {};
+    if (n < N) v = *(const h16x8*)(W + (int64_t)n * ldw + k);
+    *(h16x8*)(Wf + p * 8) = v;
+}
+
+void launch_frag_pack(const h16* W, int64_t ldw, int N, int K, h16* Wf, hipStream_t s) {
+    const int64_t pieces = (int64_t)((N + 15) / 16) * (K / 32) * 64;
+    frag_pack_kernel<<<(unsigned)((pieces + 255) / 256), 256, 0, s>>>(W, ldw, N, K, Wf, pieces);
 }
 
 int tiled_ksplit(int M, int N, int K) {

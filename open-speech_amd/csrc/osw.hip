@@ -91,6 +91,9 @@ struct Tensor {
     int64_t numel = 0;
     bool f16 = true;
     bool set = false;
+    // a decoder matrix the skinny GEMM streams: N x K, with a fragment-major copy in the
+    // tensor "<name>.frag" (GemmArgs::Wf), repacked whenever the matrix is written
+    int frag_n = 0, frag_k = 0;
 };
 
 template <typename T>
@@ -366,6 +369,26 @@ void build_weight_table(osw_ctx* c) {
     }
     add_tensor(c, "dec.lnpost.g", Dd, false);
     add_tensor(c, "dec.lnpost.b", Dd, false);
+    // fragment-major copies of what the skinny decoder GEMMs stream (+ 0.3 GB at turbo):
+    // measured on the 133 MB logits matrix (tools/gemv_probe.hip), the 1-KB contiguous
+    // fragment loads stream 5.2-5.4 TB/s against 3.9-4.2 TB/s for 16 rows x 64 B
+    auto frag = [&](const std::string& n, int64_t N, int64_t K) {
+        Tensor& t = c->w[n];
+        t.frag_n = (int)N;
+        t.frag_k = (int)K;
+        add_tensor(c, n + ".frag", (N + 15) / 16 * 16 * K, true);
+        c->w[n + ".frag"].set = true;  // derived: written by pack_frag
+    };
+    frag("dec.tok", d.n_vocab, Dd);
+    for (int i = 0; i < d.n_text_layer; ++i) {
+        const std::string p = "dec.l" + std::to_string(i);
+        frag(p + ".qkv.w", 3 * Dd, Dd);
+        frag(p + ".o.w", Dd, Dd);
+        frag(p + ".xq.w", Dd, Dd);
+        frag(p + ".xo.w", Dd, Dd);
+        frag(p + ".fc1.w", 4 * Dd, Dd);
+        frag(p + ".fc2.w", Dd, 4 * Dd);
+    }
 
     // one arena, every tensor 256-B aligned
     size_t total = 0;
@@ -397,6 +420,20 @@ Tensor& W(osw_ctx* c, const std::string& n) {
 }
 const h16* WH(osw_ctx* c, const std::string& n) { return (const h16*)W(c, n).ptr; }
 const float* WF(osw_ctx* c, const std::string& n) { return (const float*)W(c, n).ptr; }
+// the fragment-major copy of a decoder matrix (GemmArgs::Wf); OSW_NO_WFRAG=1: row-major (A/B)
+const h16* WFR(osw_ctx* c, const std::string& n) {
+    static const bool off = getenv("OSW_NO_WFRAG") != nullptr;
+    if (off) return nullptr;
+    auto it = c->w.find(n + ".frag");
+    return it == c->w.end() ? nullptr : (const h16*)it->second.ptr;
+}
+// rewrite the fragment-major copy after the matrix was written (on the context's stream)
+void pack_frag(osw_ctx* c, const std::string& n) {
+    const Tensor& t = W(c, n);
+    if (!t.frag_n) return;
+    launch_frag_pack((const h16*)t.ptr, t.frag_k, t.frag_n, t.frag_k, (h16*)W(c, n + ".frag").ptr, c->stream);
+    HIPCHK(hipGetLastError());
+}
 
 // --------------------------- mel constants ---------------------------------
 double hz_to_mel(double f) {
@@ -686,8 +723,9 @@ void decoder_step_fused(osw_ctx* c, int nb, int group, bool gather, const SelFus
     float* xs[2] = {c->xd, c->xd2};
     float* ps[2] = {c->part, c->part2};
     int xi = 0, last = 1, ks = 0;  // residual buffer holding x; slab buffer of the last GEMM
-    auto gemm = [&](const h16* A, const h16* Wt, int N, int K) {
-        GemmArgs g = gemm_plain(A, D, Wt, nullptr, nb, N, K, nullptr, 0, EPI_F32);
+    auto gemm = [&](const h16* A, const std::string& w, int N, int K) {
+        GemmArgs g = gemm_plain(A, D, WH(c, w), nullptr, nb, N, K, nullptr, 0, EPI_F32);
+        g.Wf = WFR(c, w);
         g.A_lo = A ? A + lo_d : nullptr;
         return g;
     };
@@ -702,11 +740,11 @@ void decoder_step_fused(osw_ctx* c, int nb, int group, bool gather, const SelFus
         return pa;
     };
     auto plain = [&](const h16* A, const std::string& w, int N, int K) {
-        ks = launch_gemm_skinny_partial(gemm(A, WH(c, w), N, K), ps[last ^ 1], c->stream);
+        ks = launch_gemm_skinny_partial(gemm(A, w, N, K), ps[last ^ 1], c->stream);
         last ^= 1;
     };
     auto fused = [&](int pro, const ProArgs& pa, const std::string& w, int N, int K) {
-        ks = launch_gemm_skinny_pro(gemm(nullptr, WH(c, w), N, K), pro, pa, false, ps[last ^ 1], c->stream);
+        ks = launch_gemm_skinny_pro(gemm(nullptr, w, N, K), pro, pa, false, ps[last ^ 1], c->stream);
         last ^= 1;
     };
     for (int l = 0; l < L; ++l) {
@@ -730,7 +768,7 @@ void decoder_step_fused(osw_ctx* c, int nb, int group, bool gather, const SelFus
         fused(PRO_GELU, pg, p + ".fc2.w", D, 4 * D);
     }
     const std::string pl = "dec.l" + std::to_string(L - 1);
-    GemmArgs gl = gemm(nullptr, WH(c, "dec.tok"), d.n_vocab, D);
+    GemmArgs gl = gemm(nullptr, "dec.tok", d.n_vocab, D);
     gl.C = c->logits;
     gl.ldc = d.n_vocab;
     ProArgs pl_args = resln(WF(c, pl + ".fc2.b"), "dec.lnpost", false);
@@ -758,7 +796,8 @@ bool decoder_step(osw_ctx* c, int nb, int group, bool gather, const SelFuse* sf 
     // logits stay within 1e-3 of an fp32 decoder); lo = hi + R rows
     const int64_t lo_d = (int64_t)c->R * D, lo_4d = (int64_t)c->R * 4 * D;
     // <= 64 rows: split-K skinny GEMM; more (beam search): see below
-    auto partial = [&](const h16* A, int lda, const h16* Wt, int N, int K) {
+    auto partial = [&](const h16* A, int lda, const std::string& w, int N, int K) {
+        const h16* Wt = WH(c, w);
         const int64_t lo = lda == 4 * D ? lo_4d : lo_d;
         // > 64 rows, N > 1536: 128x128 split-K tiles; N <= 1536: skinny row groups (measured
         // at 320 rows: N = 1280 11.4 vs 12.8 us, N = 3840 17.9 vs 12.8, N = 5120 21.7 vs 20.4)
@@ -772,6 +811,7 @@ bool decoder_step(osw_ctx* c, int nb, int group, bool gather, const SelFuse* sf 
             return ks;
         }
         GemmArgs g = gemm_plain(A, lda, Wt, nullptr, nb, N, K, nullptr, 0, EPI_F32);
+        g.Wf = WFR(c, w);
         g.A_lo = A + lo;
         REQUIRE((int64_t)skinny_ksplit(N, K) * nb * N <= c->part_floats, "split-K workspace too small");
         return launch_gemm_skinny_partial(g, c->part, c->stream);
@@ -788,25 +828,25 @@ bool decoder_step(osw_ctx* c, int nb, int group, bool gather, const SelFuse* sf 
                         WH(c, "dec.tok"), WF(c, "dec.pos"), c->cur_tok, c->pos, ctx, d.n_vocab, c->stream);
     for (int l = 0; l < L; ++l) {
         const std::string p = "dec.l" + std::to_string(l);
-        int ks = partial(c->xdn, D, WH(c, p + ".qkv.w"), 3 * D, D);
+        int ks = partial(c->xdn, D, p + ".qkv.w", 3 * D, D);
         launch_dec_self_attn(c->part, ks, WF(c, p + ".qkv.b"), c->kc + l * kv_layer, c->vc + l * kv_layer, c->pos, nb,
                              H, ctx, c->dattn, lo_d, gather ? c->anc : nullptr, group, c->sel, c->stream);
-        ks = partial(c->dattn, D, WH(c, p + ".o.w"), D, D);
+        ks = partial(c->dattn, D, p + ".o.w", D, D);
         launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".o.b"), c->xd, WF(c, p + ".ln2.g"), WF(c, p + ".ln2.b"),
                             c->xdn, lo_d, nullptr, nullptr, nullptr, nullptr, ctx, d.n_vocab, c->stream);
-        ks = partial(c->xdn, D, WH(c, p + ".xq.w"), D, D);
+        ks = partial(c->xdn, D, p + ".xq.w", D, D);
         {
             Timed t(c, CL_XATTN, 2.0 * nb * H * (double)T_ENC * 64 * 2);
             launch_dec_cross_attn(c->part, ks, WF(c, p + ".xq.b"), c->XKV + (2 * l) * xkv_which,
                                   c->XKV + (2 * l + 1) * xkv_which, nb, H, T_ENC, group, c->dattn, lo_d, c->xws,
                                   c->xticket, c->sel, c->stream);
         }
-        ks = partial(c->dattn, D, WH(c, p + ".xo.w"), D, D);
+        ks = partial(c->dattn, D, p + ".xo.w", D, D);
         launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".xo.b"), c->xd, WF(c, p + ".ln3.g"), WF(c, p + ".ln3.b"),
                             c->xdn, lo_d, nullptr, nullptr, nullptr, nullptr, ctx, d.n_vocab, c->stream);
         // (a whole-K fc1 with the GELU epilogue fused has only N/64 = 80 workgroups at
         // turbo: 22.7 us vs 9.6 + 4.7 us for split-K + reduce, measured)
-        ks = partial(c->xdn, D, WH(c, p + ".fc1.w"), 4 * D, D);
+        ks = partial(c->xdn, D, p + ".fc1.w", 4 * D, D);
         const float* fc2_part = c->part;
         if (gelu_pro) {
             // <= 8 rows: the GELU reduce is fc2's prologue (each workgroup reduces only its own
@@ -814,17 +854,19 @@ bool decoder_step(osw_ctx* c, int nb, int group, bool gather, const SelFuse* sf 
             ProArgs pg{};
             pg.part = c->part; pg.ks = ks; pg.bias = WF(c, p + ".fc1.b");
             GemmArgs g = gemm_plain(nullptr, D, WH(c, p + ".fc2.w"), nullptr, nb, D, 4 * D, nullptr, 0, EPI_F32);
+            g.Wf = WFR(c, p + ".fc2.w");
             ks = launch_gemm_skinny_pro(g, PRO_GELU, pg, false, c->part2, c->stream);
             fc2_part = c->part2;
         } else {
             launch_dec_reduce_gelu(c->part, ks, nb, 4 * D, WF(c, p + ".fc1.b"), c->dh, lo_4d, c->stream);
-            ks = partial(c->dh, 4 * D, WH(c, p + ".fc2.w"), D, 4 * D);
+            ks = partial(c->dh, 4 * D, p + ".fc2.w", D, 4 * D);
         }
         const std::string nx = l + 1 < L ? "dec.l" + std::to_string(l + 1) + ".ln1" : std::string("dec.lnpost");
         launch_dec_resid_ln(fc2_part, ks, nb, D, WF(c, p + ".fc2.b"), c->xd, WF(c, nx + ".g"), WF(c, nx + ".b"), c->xdn,
                             lo_d, nullptr, nullptr, nullptr, nullptr, ctx, d.n_vocab, c->stream);
     }
     GemmArgs gl = gemm_plain(c->xdn, D, WH(c, "dec.tok"), nullptr, nb, d.n_vocab, D, c->logits, d.n_vocab, EPI_F32);
+    gl.Wf = WFR(c, "dec.tok");  // used by the skinny kernel (< 24 rows); the wide kernel reads W
     gl.A_lo = c->xdn + lo_d;
     run_gemm(c, gl, 0);
     return false;
@@ -1360,6 +1402,8 @@ int osw_set_weight(osw_ctx* c, const char* name, const void* host, int64_t nbyte
             REQUIRE(nbytes == t.numel * (t.f16 ? 2 : 4), "tensor " + nm + ": wrong byte count");
             HIPCHK(hipMemcpy(t.ptr, host, nbytes, hipMemcpyHostToDevice));
         }
+        pack_frag(c, nm);
+        HIPCHK(hipStreamSynchronize(c->stream));
         t.set = true;
     });
 }
@@ -1389,6 +1433,7 @@ int osw_init_weight_uniform(osw_ctx* c, const char* name, uint64_t seed, int64_t
         launch_init_uniform(t.ptr, t.f16, t.numel, hash_stream_key(seed, stream), scale, offset, zero_lo, zero_hi,
                             c->stream);
         HIPCHK(hipGetLastError());
+        pack_frag(c, name);
         HIPCHK(hipStreamSynchronize(c->stream));
         t.set = true;
     });

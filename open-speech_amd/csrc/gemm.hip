@@ -1390,8 +1390,11 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
             Ap[PRO ? 1 : 0][r][c] = (h16)(y - (float)h);
         };
         // all slab loads of the row in one round trip (24 covers fc2's 20 slabs)
+        // (the fused-selection logits GEMM: 10 per batch, two round trips for fc2's 20 slabs,
+        // so its VGPRs fit 4 workgroups per CU and its 811 workgroups run in one round)
+        constexpr int KBIG = SEL ? 10 : 24;
         if (pa.ln.ks <= 8) resln_rows<PRO_ROWS, 8>(pa.ln, 0, g.M, wx, pred, put);
-        else resln_rows<PRO_ROWS, 24>(pa.ln, 0, g.M, wx, pred, put);
+        else resln_rows<PRO_ROWS, KBIG>(pa.ln, 0, g.M, wx, pred, put);
         __syncthreads();
     } else if constexpr (PRO == PRO_GELU) {
         const int64_t slab = (int64_t)g.M * g.K;

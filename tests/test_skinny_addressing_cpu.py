@@ -49,6 +49,62 @@ def kernel_consts(MT, LO):         # gemm_skinny_kernel<MT, ..., LO, PRO_NONE>
     return CK, CKK, CPR, RPP, SWM, ROWS, APIECES
 
 
+def frag_index(N, K, n, k):
+    """launch_frag_pack: element (n, k) of W[N][K] -> its index in the fragment-major copy
+    [ceil(N/16)][K/32][64 lanes][8]: lane = (n % 16) + 16 ((k % 32) // 8)."""
+    lane = (n % 16) + 16 * ((k % 32) // 8)
+    return (((n // 16) * (K // 32) + k // 32) * 64 + lane) * 8 + k % 8
+
+
+def audit_frag(N, K, nb, k0, st):
+    """gemm_skinny_kernel with GemmArgs::Wf: the lane's 16 B at Wf + ((blk K/32 + k0/32) 512
+    + 8 lane) + 512 st hold W[nb + lane % 16][k0 + 8 (lane // 16) + 32 st .. +8] for every
+    column < N (a block past the padded N is clamped; its columns are discarded)."""
+    npad = (N + 15) // 16 * 16
+    lane = np.arange(64)
+    blk = min(nb, npad - 16) >> 4
+    e = ((blk * (K >> 5) + (k0 >> 5)) * 512 + lane * 8) + 512 * st
+    assert e.min() >= 0 and (e + 7).max() < npad * K
+    n = nb + (lane & 15)
+    k = k0 + 8 * (lane >> 4) + 32 * st
+    ok = (n < N) & (nb < npad)
+    np.testing.assert_array_equal(e[ok], frag_index(N, K, n[ok], k[ok]))
+
+
+def test_frag_pack_layout():
+    """The pack kernel's mapping (one thread per 16-B piece p: lane = p % 64, step =
+    (p // 64) % (K/32), block = p // (64 K/32)) is the inverse of frag_index, and a
+    wave's k32 fragment is one contiguous 1-KB piece."""
+    rng = np.random.default_rng(0)
+    for N, K in ((37, 64), (51866 % 4096 + 5, 128), (96, 256)):
+        W = rng.integers(0, 60000, size=(N, K)).astype(np.uint16)
+        npad = (N + 15) // 16 * 16
+        pieces = npad // 16 * (K // 32) * 64
+        Wf = np.zeros(pieces * 8, np.uint16)
+        p = np.arange(pieces)
+        lane, t = p & 63, p >> 6
+        st, blk = t % (K // 32), t // (K // 32)
+        n = blk * 16 + (lane & 15)
+        k = st * 32 + 8 * (lane >> 4)
+        for j in range(8):
+            Wf[p * 8 + j] = np.where(n < N, W[np.minimum(n, N - 1), k + j], 0)
+        nn, kk = np.meshgrid(np.arange(N), np.arange(K), indexing="ij")
+        np.testing.assert_array_equal(Wf[frag_index(N, K, nn, kk)], W)
+        assert Wf.size == npad * K
+        pad = (p * 8)[(n >= N)]            # pieces of the padded columns hold zeros
+        assert all(not Wf[q:q + 8].any() for q in pad)
+
+
+def test_frag_logits_addressing():
+    """The batch-1 logits GEMM (direct, kc = K, N = the vocabulary) through Wf."""
+    for dims in (D.MICRO_TEST, D.TINY_TEST, D.LARGE_V3_TURBO):
+        N, K = dims.n_vocab, dims.n_text_state
+        for bx in sorted({0, (N + 63) // 64 - 2, (N + 63) // 64 - 1}):
+            for wave in range(4):
+                for st in (0, K // 32 - 1):
+                    audit_frag(N, K, bx * 64 + wave * 16, 0, st)
+
+
 def audit(M, N, K, lo, R):
     """One launch: activations [R or 2R][lda = K] (hi rows, then lo rows R later, as
     decoder_step lays out xdn / dattn / dh), weights [N][K], slabs [ks][M][N]."""
@@ -76,6 +132,7 @@ def audit(M, N, K, lo, R):
                         st = min(c * CK + u, nsteps - 1)
                         e = n * K + k0 + 8 * gq + 32 * st
                         assert e.min() >= 0 and (e + 7).max() < N * K
+                        audit_frag(N, K, nb, k0, st)
                 for bz in range(nz):
                     mb = bz * ROWS
                     # staging: LDS[row][(lane % CPR) * 8 ..] <- A[gr][k0 + min(kk + acl, kc - 8) ..]

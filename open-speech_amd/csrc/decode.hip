@@ -537,7 +537,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
 // Wave w: keys 48w .. 48w+47 (3 tiles of 16) for the scores and for P·V over all 64 dims
 // (one max for the workgroup, exchanged before the exponentials); the 4 waves' P·V sums
 // meet in LDS in fixed order.
-template <int NB>
+// KLDS: K arrives like V, 8 rows x 128 B per wave-instruction (whole cache lines), and is
+// staged through the V image into the MFMA A layout; otherwise each lane loads its A
+// fragment straight from HBM (16 keys x 64 B per wave-instruction: every line is touched
+// by two instructions, the pattern that streamed the logits matrix at 3.95 instead of
+// 5.4 TB/s, tools/gemv_probe.hip).  Same K elements in the same fragments: same results.
+template <int NB, bool KLDS = true>
 __global__ __launch_bounds__(256) void dec_xattn_mfma_kernel(const float* __restrict__ part, int ks,
                                                              const float* __restrict__ bias,
                                                              const h16* __restrict__ xk, const h16* __restrict__ xv,
@@ -583,13 +588,21 @@ __global__ __launch_bounds__(256) void dec_xattn_mfma_kernel(const float* __rest
         qb[k] = part[min(wv + 4, ks - 1) * slab + off];
     }
     // K fragments of this wave's 3 key tiles (A operand), nontemporal, clamped to the chunk
-    h16x8 kf[3][2];
+    h16x8 kf[3][2], kr[6];
+    if constexpr (KLDS) {
 #pragma unroll
-    for (int t = 0; t < 3; ++t) {
-        const int key = k0 + min(16 * (3 * wv + t) + li, nk - 1);
+        for (int i = 0; i < 6; ++i) {
+            const int r = (i * 4 + wv) * 8 + (lane >> 3);
+            kr[i] = __builtin_nontemporal_load((const h16x8*)(xk + hoff + (int64_t)(k0 + min(r, nk - 1)) * HD + 8 * (lane & 7)));
+        }
+    } else {
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
-            kf[t][s] = __builtin_nontemporal_load((const h16x8*)(xk + hoff + (int64_t)key * HD + 32 * s + 8 * g));
+        for (int t = 0; t < 3; ++t) {
+            const int key = k0 + min(16 * (3 * wv + t) + li, nk - 1);
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+                kf[t][s] = __builtin_nontemporal_load((const h16x8*)(xk + hoff + (int64_t)key * HD + 32 * s + 8 * g));
+        }
     }
     // V chunk: 24 pieces of 8 rows x 128 B, 6 per wave, into registers now and into LDS
     // (16-B chunk XOR-swizzled by row) once they land.  Plain loads, not global_load_lds:
@@ -604,6 +617,15 @@ __global__ __launch_bounds__(256) void dec_xattn_mfma_kernel(const float* __rest
 #pragma unroll
     for (int k = 0; k < NB; ++k) red[wv][k][lane] = (has_a ? qa[k] : 0.f) + (has_b ? qb[k] : 0.f);
     bsh[wv][lane] = bq;  // every wave, through LDS: hipcc cannot sink the load past the K/V loads
+    if constexpr (KLDS) {
+        // the K chunk into the V image (V goes there after the scores: the max exchange's
+        // barrier below orders every wave's fragment reads before the V stores)
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const int r = (i * 4 + wv) * 8 + (lane >> 3);
+            *(h16x8*)&Vl[r * HD + (((lane & 7) ^ ((r >> 1) & 7)) * 8)] = kr[i];
+        }
+    }
     lds_barrier();
     if (wv == 0) {
 #pragma unroll
@@ -619,6 +641,14 @@ __global__ __launch_bounds__(256) void dec_xattn_mfma_kernel(const float* __rest
     }
     lds_barrier();
     const h16x8 qf0 = *(const h16x8*)&qsh[li][8 * g], qf1 = *(const h16x8*)&qsh[li][32 + 8 * g];
+    if constexpr (KLDS) {
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const int r = 16 * (3 * wv + t) + li;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) kf[t][s] = *(const h16x8*)&Vl[r * HD + (((4 * s + g) ^ ((r >> 1) & 7)) * 8)];
+        }
+    }
     // scores: lane holds key 16(3wv + t) + 4g + i of row li
     f32x4 sc[3];
     float mx = -INFINITY;
@@ -1186,8 +1216,14 @@ void launch_dec_cross_attn(const float* part, int ks, const float* bias, const h
     const unsigned grid = (unsigned)(((W * H + 7) / 8) * 8 * XCH);
     static const bool valu_beam = std::getenv("OSW_XATTN_VALU") != nullptr;  // A/B switch
     if (beam > 1 && !valu_beam && ks <= 8) {
-        if (beam <= 5) dec_xattn_mfma_kernel<5><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off, st);
-        else dec_xattn_mfma_kernel<8><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off, st);
+        static const bool kdirect = std::getenv("OSW_XATTN_KDIRECT") != nullptr;  // A/B switch
+        if (kdirect) {
+            if (beam <= 5) dec_xattn_mfma_kernel<5, false><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off, st);
+            else dec_xattn_mfma_kernel<8, false><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off, st);
+        } else {
+            if (beam <= 5) dec_xattn_mfma_kernel<5><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off, st);
+            else dec_xattn_mfma_kernel<8><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off, st);
+        }
         return;
     }
     switch (beam) {

@@ -1206,7 +1206,7 @@ __device__ __forceinline__ void fused_select_row(float x, int col, bool valid, c
 }
 
 template <int MT, bool DIRECT, int EPI, bool LO, int PRO = PRO_NONE, bool SEL = false>
-__global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, float* __restrict__ part, ProArgs pa) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL ? 4 : 1, 8))) void gemm_skinny_kernel(GemmArgs g, int kc, float* __restrict__ part, ProArgs pa) {
     // Workgroup = 64 columns x one kc-deep K range; wave = 16 columns.  The
     // activation rows (M <= 64) of each CKK-deep K chunk are staged ONCE per
     // workgroup into LDS by global_load_lds (row-XOR swizzle on the 16-B chunk ->
@@ -1381,6 +1381,10 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
     h16x8 wa[CK], wb[CK];
     loadW(wa, 0);
     stageA(0, 0);
+    // the fused-selection logits GEMM (5 chunks): the second chunk goes out before the
+    // prologue too (GemmArgs::preload_w), so two chunks stream while the row is normalised
+    const bool wb_early = SEL && g.preload_w && nch > 1;
+    if (wb_early) loadW(wb, 1);
     if constexpr (PRO == PRO_RESLN) {
         // every workgroup normalises all rows (a few KB from L2); one stores x'
         const bool wx = blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0;
@@ -1392,7 +1396,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
         // all slab loads of the row in one round trip (24 covers fc2's 20 slabs)
         // (the fused-selection logits GEMM: 10 per batch, two round trips for fc2's 20 slabs,
         // so its VGPRs fit 4 workgroups per CU and its 811 workgroups run in one round)
-        constexpr int KBIG = SEL ? 10 : 24;
+        constexpr int KBIG = SEL ? 8 : 24;
         if (pa.ln.ks <= 8) resln_rows<PRO_ROWS, 8>(pa.ln, 0, g.M, wx, pred, put);
         else resln_rows<PRO_ROWS, KBIG>(pa.ln, 0, g.M, wx, pred, put);
         __syncthreads();
@@ -1419,7 +1423,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g, int kc, fl
     }
     for (int c = 0; c < nch; c += 2) {
         if (c + 1 < nch) {
-            loadW(wb, c + 1);
+            if (!(wb_early && c == 0)) loadW(wb, c + 1);
             stageA(1, c + 1);
             wait_vmcnt<INFLIGHT>();
         } else {
@@ -1717,11 +1721,14 @@ int launch_gemm_skinny_partial(const GemmArgs& g0, float* part, hipStream_t s) {
 // Fused small-batch form (<= PRO_ROWS hi/lo rows for PRO_RESLN, <= GELU_ROWS for PRO_GELU):
 // the operand is built by the prologue (resln.h).  direct: one K range, EPI_F32 straight into g.C (the logits); otherwise the
 // split-K slabs into part, as launch_gemm_skinny_partial.  Returns ksplit.
-int launch_gemm_skinny_pro(const GemmArgs& g, int pro, const ProArgs& pa, bool direct, float* part, hipStream_t s,
+int launch_gemm_skinny_pro(const GemmArgs& g0, int pro, const ProArgs& pa, bool direct, float* part, hipStream_t s,
                            bool select) {
+    GemmArgs g = g0;
     const int ks = direct ? 1 : skinny_ksplit(g.N, g.K);
     const dim3 grid((g.N + 63) / 64, ks, 1);
     const int kc = g.K / ks;
+    static const bool wb_late = getenv("OSW_PRO_WB_LATE") != nullptr;  // A/B switch
+    g.preload_w = wb_late ? 0 : 1;
     if (pro == PRO_GELU ? g.M > GELU_ROWS || kc > GELU_KC : g.M > PRO_ROWS)
         throw std::invalid_argument("fused GEMM prologue: rows or K range exceed its LDS image");
     if (select) {

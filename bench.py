@@ -42,7 +42,9 @@ MFMA_F16_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA spec
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--steps", type=int, default=20,
+                    help="timed 64-clip steps; the first ~3 fill the lanes' pipeline (measured, r03_ac: "
+                         "6 steps 4942, 12 steps 5043, 24 steps 5099 audio-s/s)")
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=64, help="30 s clips per GPU per step")
     ap.add_argument("--lanes", type=int, default=3,

@@ -58,7 +58,10 @@ __device__ __forceinline__ h16x8 ld8(const h16* p) {
 // soff[p] = anc[p] - self (0 for the newest key, always this row's own), staged in LDS by
 // the caller before its slab reduction's barrier, so the ancestry costs no round trip of
 // its own.
-template <int MAXK, bool GATHER = false, bool NT = !GATHER>
+// VPRE (the self-attention, MAXK = 448): each 256-key block's V pieces are issued with its K
+// pieces, so the P·V pass finds them landed (one HBM round trip per block instead of two);
+// the V pieces stay in registers across the softmax reductions.
+template <int MAXK, bool GATHER = false, bool NT = !GATHER, bool VPRE = false>
 __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ K, const h16* __restrict__ V,
                            int n_keys, h16* __restrict__ out, int64_t lo_off, const int* soff = nullptr,
                            int64_t slot_stride = 0) {
@@ -83,6 +86,7 @@ __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ 
 #pragma unroll
     for (int i = 0; i < 8; ++i) q[i] = qs[8 * c8 + i];
     float mx = -INFINITY;
+    h16x8 vpre[VPRE ? NBLK : 1][8];
     // 256 keys (8 loads per lane) per round trip: at most 2 for 448 keys
 #pragma unroll
     for (int blk = 0; blk < NBLK; ++blk) {
@@ -93,6 +97,10 @@ __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ 
         for (int u = 0; u < 8; ++u) {
             const int key = min(base + u * 32 + kg, n_keys - 1);
             kv[u] = ld8<NT>(krow(K, key) + 8 * c8);
+        }
+        if constexpr (VPRE) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) vpre[blk][u] = ld8<NT>(krow(V, min(base + u * 32 + kg, n_keys - 1)) + 8 * c8);
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
@@ -129,7 +137,10 @@ __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ 
         h16x8 v[8];
         float p[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = ld8<NT>(krow(V, min(j + 32 * u, n_keys - 1)) + 8 * c8);
+        for (int u = 0; u < 8; ++u) {
+            if constexpr (VPRE) v[u] = vpre[blk][u];
+            else v[u] = ld8<NT>(krow(V, min(j + 32 * u, n_keys - 1)) + 8 * c8);
+        }
 #pragma unroll
         for (int u = 0; u < 8; ++u) p[u] = j + 32 * u < n_keys ? sc[j + 32 * u] : 0.f;
 #pragma unroll
@@ -200,7 +211,7 @@ __device__ __forceinline__ void reduce_qkv(const float* __restrict__ part, int k
 // first K/V batch before the slab reduction left the batch-1 p50 unchanged, measured.)
 // GATHER (beam rows): the row's ancestry is loaded before the slab reduction and staged in
 // LDS behind its barrier, so it lands with the slabs (one round trip) instead of after.
-template <bool GATHER>
+template <bool GATHER, bool VPRE>
 __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restrict__ part, int ks,
                                                             const float* __restrict__ bias, h16* __restrict__ kcache,
                                                             h16* __restrict__ vcache, const int* __restrict__ pos_ptr,
@@ -250,9 +261,10 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
     __threadfence_block();
     __syncthreads();
     if constexpr (GATHER)
-        attend_one<448, true>(q16, kc, vc, pos + 1, out + (int64_t)b * D + h * HD, lo_off, soff, (int64_t)H * ctx * HD);
+        attend_one<448, true, false, VPRE>(q16, kc, vc, pos + 1, out + (int64_t)b * D + h * HD, lo_off, soff,
+                                           (int64_t)H * ctx * HD);
     else
-        attend_one<448>(q16, kc, vc, pos + 1, out + (int64_t)b * D + h * HD, lo_off);
+        attend_one<448, false, true, VPRE>(q16, kc, vc, pos + 1, out + (int64_t)b * D + h * HD, lo_off);
 }
 
 // grid H*B (flattened): q = Σ split-K partials of the cross-attention q projection
@@ -792,6 +804,15 @@ static_assert(BEAM_SLICES * 256 * TOPK_VPT >= SEL_SPLIT * 4096, "osw.hip admits 
 // already -inf (all scores tie at -inf), and two different logits whose scores round to
 // the same float at the top-2K cutoff (here the larger logit wins, there the lower flat
 // index); CTranslate2's tie order on such inputs is unpinned (no fixture covers it).
+//
+// FAST (default): the K2 pops (a block barrier each) run only where a cheaper exact form
+// cannot: each wave finds the K2-th largest of its 64 lane maxima (wave-only pops, no
+// barrier), T = the largest of the 4.  At least K2 allowed entries are >= T (the popped
+// lanes' maxima), so the slice's top K2 lie in S = {allowed live entries >= T}; S is
+// gathered in LDS and each member's rank under (key desc, token asc) -- the pops' order --
+// is counted directly.  Falls back to the pops when T = -inf (fewer than K2 finite
+// allowed entries in every wave) or |S| > 256.
+template <bool FAST>
 __device__ __forceinline__ void beam_slice_body(const float* __restrict__ logits, const SelParams& P, int step,
                                                 const unsigned* __restrict__ supmask, const SelState& s,
                                                 SelPart* __restrict__ parts, BeamCand* __restrict__ cand) {
@@ -883,8 +904,69 @@ __device__ __forceinline__ void beam_slice_body(const float* __restrict__ logits
             }
         }
     };
-    pops(okA, outA);
-    if (hi > P.tb) pops(okB, outB);
+    constexpr int SCAP = 256;
+    __shared__ BeamCand sset[2][SCAP];
+    __shared__ float tw[2][4];
+    __shared__ int scnt[2];
+    // block-uniform result: true = out[0..K2) written from S
+    auto fast = [&](unsigned ok, BeamCand* out, int L) -> bool {
+        const int lane = tid & 63;
+        const unsigned al = ok & live;
+        float lm = -INFINITY;
+#pragma unroll
+        for (int u = 0; u < TOPK_VPT; ++u)
+            if ((al >> u) & 1u) lm = fmaxf(lm, xv[u]);
+        ArgMax c{lm, lane};
+        float t = INFINITY;
+        for (int r = 0; r < K2; ++r) {
+            ArgMax a = c;
+            auto stp = [&](auto o) {
+                constexpr int O = decltype(o)::value;
+                a = amax(a, ArgMax{xor_lane<O>(a.v), xor_lane<O>(a.i)});
+            };
+            stp(IC<32>{}), stp(IC<16>{}), stp(IC<8>{}), stp(IC<4>{}), stp(IC<2>{}), stp(IC<1>{});
+            t = a.v;
+            if (lane == a.i) c.v = -INFINITY;
+        }
+        if (lane == 0) tw[L][tid >> 6] = t;
+        if (tid == 0) scnt[L] = 0;
+        __syncthreads();
+        const float T = fmaxf(fmaxf(tw[L][0], tw[L][1]), fmaxf(tw[L][2], tw[L][3]));
+        if (T == -INFINITY) return false;
+        unsigned qm = 0;
+#pragma unroll
+        for (int u = 0; u < TOPK_VPT; ++u)
+            if (((al >> u) & 1u) && xv[u] >= T) qm |= 1u << u;
+        if (qm) {
+            int bi = lo + tid;
+            asm volatile("" : "+v"(bi));  // token ids not shared with (kept live for) the pops
+            int k = atomicAdd(&scnt[L], __popc(qm));
+#pragma unroll
+            for (int u = 0; u < TOPK_VPT; ++u)
+                if ((qm >> u) & 1u) {
+                    if (k < SCAP) sset[L][k] = BeamCand{xv[u], bi + u * 256};
+                    ++k;
+                }
+        }
+        __syncthreads();
+        const int n = scnt[L];
+        if (n > SCAP) return false;
+        for (int i = tid; i < n; i += 256) {
+            const BeamCand e = sset[L][i];
+            int rank = 0;
+#pragma unroll 1
+            for (int j = 0; j < n; ++j) {
+                const BeamCand f = sset[L][j];
+                rank += (f.s > e.s || (f.s == e.s && f.i < e.i)) ? 1 : 0;
+            }
+            if (rank < K2) out[rank] = e;
+        }
+        return true;
+    };
+    if (!FAST || !fast(okA, outA, 0)) pops(okA, outA);
+    if (hi > P.tb) {
+        if (!FAST || !fast(okB, outB, 1)) pops(okB, outB);
+    }
     else if (tid < K2) outB[tid] = BeamCand{-INFINITY, INT_MAX};  // no timestamps in this slice
     __syncthreads();
     if (tid == 0) {
@@ -912,7 +994,8 @@ __device__ __forceinline__ void beam_slice_body(const float* __restrict__ logits
 // compiles only its own path: the greedy kernel carries neither the Gumbel keys nor the
 // beam candidate lists (47 VGPRs, so it fits beside another lane's encoder workgroup).
 template <int MODE>
-__global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ logits, SelParams P,
+// waves_per_eu(6): <= 80 VGPRs (the beam form needs 81 unbounded), so it fits beside an encoder GEMM workgroup
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void select_kernel(const float* __restrict__ logits, SelParams P,
                                                      int* __restrict__ pos_ptr, const unsigned* __restrict__ supmask,
                                                      const int* __restrict__ prompt, SelPart* __restrict__ parts,
                                                      SelState* __restrict__ st, int* __restrict__ cur_tok,
@@ -920,13 +1003,13 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ l
                                                      int* __restrict__ arrive, int* __restrict__ ticket, int bump,
                                                      BeamCand* __restrict__ cand) {
     const int step = *pos_ptr;
-    if (MODE == 2 && P.beam > 1) {
+    if ((MODE == 2 || MODE == 3) && P.beam > 1) {
         const SelState s = st[blockIdx.x];
         if (sel_mode(P, step, s) == SEL_SAMPLE) {  // the same for every slice of the row
             // beam rows' sampling steps: statistics + candidates in one pass; nothing to
             // finalise here (beam_update picks), so no ticket
             if (step == P.prompt_len - 1 && blockIdx.x % P.beam != 0) return;  // only the prompt hypothesis expands
-            beam_slice_body(logits, P, step, supmask, s, parts, cand);
+            beam_slice_body<MODE == 2>(logits, P, step, supmask, s, parts, cand);
             return;
         }
     }
@@ -1196,12 +1279,29 @@ int beam_cand_bytes(int) { return (int)sizeof(BeamCand) * BEAM_SLICES * 2 * MAXK
 void launch_dec_self_attn(const float* part, int ks, const float* bias, h16* kc, h16* vc, const int* pos, int B,
                           int H, int ctx, h16* out, int64_t lo_off, const int* anc, int group, const SelState* st,
                           hipStream_t s) {
-    if (anc)  // ctx <= 448 (osw.hip checks the context at decode)
-        dec_self_attn_kernel<true><<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, lo_off, anc,
-                                                         group, st);
-    else
-        dec_self_attn_kernel<false><<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, lo_off,
-                                                          nullptr, 1, st);
+    // V issued with K (VPRE, 139 VGPRs) only for a few rows: batch-1 p50 114.3 / 114.8 ->
+    // 113.6 / 113.4 ms greedy, 152.2 / 153.5 -> 151.6 / 151.4 ms beam 5; at 64 rows its 3
+    // waves per SIMD lose to the 7 of the 66-VGPR form (16.9 -> 20.8 us per launch, beam rows
+    // 49.0 -> 66.6 us; gpurun_out/r03_ae).  OSW_SELF_VPRE=0 / 1: never / always.
+    static const int vpre_env = [] {
+        const char* e = std::getenv("OSW_SELF_VPRE");
+        return e ? (e[0] == '1' ? 1 : 0) : -1;
+    }();
+    const bool vlate = vpre_env < 0 ? B > 8 : vpre_env == 0;
+    if (anc) {  // ctx <= 448 (osw.hip checks the context at decode)
+        if (vlate)
+            dec_self_attn_kernel<true, false><<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, lo_off,
+                                                                    anc, group, st);
+        else
+            dec_self_attn_kernel<true, true><<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, lo_off,
+                                                                   anc, group, st);
+    } else if (vlate) {
+        dec_self_attn_kernel<false, false><<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, lo_off,
+                                                                 nullptr, 1, st);
+    } else {
+        dec_self_attn_kernel<false, true><<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, lo_off,
+                                                                nullptr, 1, st);
+    }
 }
 
 void launch_dec_cross_attn(const float* part, int ks, const float* bias, const h16* xk, const h16* xv, int B, int H,
@@ -1256,7 +1356,12 @@ void launch_select(const float* logits, int rows, int* pos, const SelParams& P, 
     // arrive[0]: rows finalised this step; arrive[1 + row]: the row's slice tickets; cand:
     // the beam rows' candidate lists (beam_slice_body)
     const dim3 grid(rows, SEL_SPLIT);
-    if (P.beam > 1)
+    // OSW_BEAM_POPS=1 (A/B switch): the beam candidate lists by K2 block-wide pops everywhere
+    static const bool pops_only = std::getenv("OSW_BEAM_POPS") != nullptr;
+    if (P.beam > 1 && pops_only)
+        select_kernel<3><<<grid, 256, 0, s>>>(logits, P, pos, supmask, prompt, (SelPart*)sel_parts, st, cur_tok, tokens,
+                                               max_tokens, arrive, arrive + 1, bump ? 1 : 0, (BeamCand*)cand);
+    else if (P.beam > 1)
         select_kernel<2><<<grid, 256, 0, s>>>(logits, P, pos, supmask, prompt, (SelPart*)sel_parts, st, cur_tok, tokens,
                                                max_tokens, arrive, arrive + 1, bump ? 1 : 0, (BeamCand*)cand);
     else if (P.inv_temp > 0.f)

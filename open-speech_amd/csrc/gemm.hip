@@ -1487,44 +1487,65 @@ store:
 // 3-slot version held one per CU and ran the 406 logits tiles in two rounds:
 // 58.8 us per step).
 constexpr int WBM = 64, WBN = 128, WSL = 3;
-template <bool LO>
-__global__ __launch_bounds__(256, 2) void gemm_wide_kernel(GemmArgs g) {
+// WN = 256 (the vocabulary logits, N >= 16384, no split-K): 8 waves and a 64 x 256 tile, one
+// workgroup per CU (128 KiB of dynamic LDS).  Per 64-deep K step a workgroup stages
+// (64 rows of A, hi + lo) + WN rows of W: 256 columns stage 25 % fewer bytes per MAC than
+// 128 (at 320 beam rows the 133 MB matrix is staged 5 times either way, the activations
+// 203 instead of 406 times).  Same MFMA chain per output element: identical results.
+template <int WN>
+constexpr int wide_lds(bool lo) { return (lo ? 2 * 2 : WSL) * WBM * BK * 2 + WSL * WN * BK * 2; }
+
+template <bool LO, int WN = WBN>
+__global__ __launch_bounds__(WN * 2, WN == WBN ? 2 : 1) void gemm_wide_kernel(GemmArgs g) {
     constexpr int NIMG = LO ? 2 : 1;
     constexpr int ASL = LO ? 2 : WSL;  // A ring slots
-    __shared__ __attribute__((aligned(16))) h16 la[ASL][NIMG][WBM * BK];
-    __shared__ __attribute__((aligned(16))) h16 lw[WSL][WBN * BK];
+    constexpr int NW = WN / 32, NT = 64 * NW;  // waves, threads
+    constexpr int GA = 8 / NW;                 // A staging groups (8 rows x 64 k) per wave and image
+    h16* la;  // [ASL][NIMG][WBM * BK]
+    h16* lw;  // [WSL][WN * BK]
+    if constexpr (WN == WBN) {
+        __shared__ __attribute__((aligned(16))) h16 sa[ASL][NIMG][WBM * BK];
+        __shared__ __attribute__((aligned(16))) h16 sw[WSL][WN * BK];
+        la = &sa[0][0][0];
+        lw = &sw[0][0];
+    } else {
+        extern __shared__ __attribute__((aligned(16))) h16 smem[];
+        la = smem;
+        lw = smem + ASL * NIMG * WBM * BK;
+    }
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int n0 = blockIdx.x * WBN, m0 = blockIdx.y * WBM;
+    const int n0 = blockIdx.x * WN, m0 = blockIdx.y * WBM;
     const int kc = g.kc > 0 ? g.kc : g.K, kbeg = blockIdx.z * kc;
-    // staging: one wave-instruction fills 8 rows x 64 k (1 KiB); A 8 groups (2 per
-    // wave) per image, W 16 groups (4 per wave); the 16-B chunk is XOR-swizzled by row
-    const h16* asrc[NIMG][2];
+    // staging: one wave-instruction fills 8 rows x 64 k (1 KiB); A 8 groups (GA per
+    // wave) per image, W WN / 8 groups (4 per wave); the 16-B chunk is XOR-swizzled by row
+    const h16* asrc[NIMG][GA];
     const h16* wsrc[4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int r = (i * 4 + wave) * 8 + (lane >> 3);
+    for (int i = 0; i < GA; ++i) {
+        const int r = (i * NW + wave) * 8 + (lane >> 3);
         const int64_t gm = min(m0 + r, g.M - 1);
         asrc[0][i] = g.A + gm * g.lda + swz(r, lane & 7) * 8 + kbeg;
         if constexpr (LO) asrc[NIMG - 1][i] = g.A_lo + gm * g.lda + swz(r, lane & 7) * 8 + kbeg;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int r = (i * 4 + wave) * 8 + (lane >> 3);
+        const int r = (i * NW + wave) * 8 + (lane >> 3);
         wsrc[i] = g.W + (int64_t)min(n0 + r, g.N - 1) * g.ldw + swz(r, lane & 7) * 8 + kbeg;
     }
     auto stageA = [&](int slot, int k0) {
 #pragma unroll
         for (int im = 0; im < NIMG; ++im)
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int i = 0; i < GA; ++i)
                 __builtin_amdgcn_global_load_lds((const void*)(asrc[im][i] + k0),
-                                                 (OSW_LDS void*)&la[slot][im][(i * 4 + wave) * 8 * BK], 16, 0, 0);
+                                                 (OSW_LDS void*)&la[(slot * NIMG + im) * WBM * BK + (i * NW + wave) * 8 * BK],
+                                                 16, 0, 0);
     };
     auto stageW = [&](int slot, int k0) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-            __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + k0), (OSW_LDS void*)&lw[slot][(i * 4 + wave) * 8 * BK],
-                                             16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + k0),
+                                             (OSW_LDS void*)&lw[slot * WN * BK + (i * NW + wave) * 8 * BK], 16, 0, 0);
     };
     f32x4 acc[4][2];
 #pragma unroll
@@ -1546,7 +1567,7 @@ __global__ __launch_bounds__(256, 2) void gemm_wide_kernel(GemmArgs g) {
     for (int kt = 0; kt < nk; ++kt) {
         // tile kt has landed: younger than it are only tile kt+1's W (LO) or A+W
         if (kt + 1 < nk)
-            wait_vmcnt<LO ? 4 : 6>();
+            wait_vmcnt<LO ? 4 : 4 + GA>();
         else
             wait_vmcnt<0>();
         __syncthreads();  // every thread's tile kt has landed; the slots refilled below are no longer read
@@ -1557,7 +1578,7 @@ __global__ __launch_bounds__(256, 2) void gemm_wide_kernel(GemmArgs g) {
             if (kt + 2 < nk) { stageA((kt + 2) % WSL, (kt + 2) * BK); stageW((kt + 2) % WSL, (kt + 2) * BK); }
         }
         const int sa = kt % ASL;
-        const h16* W = lw[kt % WSL];
+        const h16* W = lw + (kt % WSL) * WN * BK;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             const int c = ks * 4 + (lane >> 4);
@@ -1567,7 +1588,7 @@ __global__ __launch_bounds__(256, 2) void gemm_wide_kernel(GemmArgs g) {
 #pragma unroll
                 for (int mi = 0; mi < 4; ++mi) {
                     const int row = mi * 16 + (lane & 15);
-                    a[im][mi] = *(const h16x8*)&la[sa][im][row * BK + swz(row, c) * 8];
+                    a[im][mi] = *(const h16x8*)&la[(sa * NIMG + im) * WBM * BK + row * BK + swz(row, c) * 8];
                 }
 #pragma unroll
             for (int ni = 0; ni < 2; ++ni) {
@@ -1586,14 +1607,14 @@ __global__ __launch_bounds__(256, 2) void gemm_wide_kernel(GemmArgs g) {
     }
     float* C = (float*)g.C + (g.kc > 0 ? (int64_t)blockIdx.z * g.M * g.ldc : 0);
     const float* bias = g.kc > 0 ? nullptr : g.bias;
-    // the 64 x 128 fp32 tile leaves through LDS (the W ring, free once every wave is past
+    // the 64 x WN fp32 tile leaves through LDS (the W ring, free once every wave is past
     // its last K tile) as 8-B device-scope (write-through) stores, 512 B contiguous per
     // wave-instruction: the MFMA layout's 4-B stores scattered over 4 rows took ~half of
     // the beam logits GEMM (66 MB of fp32 at 320 rows).  Rows stay 8-B aligned for the
     // vocabulary's row stride (51866 floats), not 16-B.
-    constexpr int TS = 2 * WBM + 2;  // LDS row stride (floats) of the 64 x 128 tile
-    static_assert(WBM * TS * 4 <= WSL * WBN * BK * 2, "the tile fits the W ring");
-    float* T = (float*)&lw[0][0];
+    constexpr int TS = WN + 2;  // LDS row stride (floats) of the 64 x WN tile
+    static_assert(WBM * TS * 4 <= WSL * WN * BK * 2, "the tile fits the W ring");
+    float* T = (float*)lw;
     __syncthreads();
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
@@ -1609,8 +1630,8 @@ __global__ __launch_bounds__(256, 2) void gemm_wide_kernel(GemmArgs g) {
         }
     __syncthreads();
 #pragma unroll 4
-    for (int f = threadIdx.x; f < WBM * WBN / 2; f += 256) {
-        const int row = f / (WBN / 2), c2 = (f % (WBN / 2)) * 2;
+    for (int f = threadIdx.x; f < WBM * WN / 2; f += NT) {
+        const int row = f / (WN / 2), c2 = (f % (WN / 2)) * 2;
         const int m = m0 + row, n = n0 + c2;
         if (m >= g.M || n >= g.N) continue;
         float* dst = C + (int64_t)m * g.ldc + n;
@@ -1624,7 +1645,27 @@ __global__ __launch_bounds__(256, 2) void gemm_wide_kernel(GemmArgs g) {
     }
 }
 
+template <bool LO>
+void launch_wide256(const GemmArgs& g, int ks, hipStream_t s) {
+    static bool attr = false;
+    constexpr int lds = wide_lds<256>(LO);
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)gemm_wide_kernel<LO, 256>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        attr = true;
+    }
+    gemm_wide_kernel<LO, 256><<<dim3((g.N + 255) / 256, (g.M + WBM - 1) / WBM, ks), 512, lds, s>>>(g);
+}
+
 void launch_wide(const GemmArgs& g, int ks, hipStream_t s) {
+    // OSW_WIDE_N128=1 (A/B switch): the logits on the 64 x 128 tile too
+    // OSW_WIDE256_ALL=1 (A/B switch): the split-K projections of beam rows on it as well
+    static const bool n128 = getenv("OSW_WIDE_N128") != nullptr;
+    static const bool all256 = getenv("OSW_WIDE256_ALL") != nullptr;
+    if (!n128 && ((ks == 1 && g.kc == 0 && g.N >= 16384) || all256)) {
+        if (g.A_lo) launch_wide256<true>(g, ks, s);
+        else launch_wide256<false>(g, ks, s);
+        return;
+    }
     const dim3 grid((g.N + WBN - 1) / WBN, (g.M + WBM - 1) / WBM, ks);
     if (g.A_lo) gemm_wide_kernel<true><<<grid, 256, 0, s>>>(g);
     else gemm_wide_kernel<false><<<grid, 256, 0, s>>>(g);

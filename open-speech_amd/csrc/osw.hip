@@ -649,7 +649,16 @@ void encode(osw_ctx* c, const osw_window* wins, int n) {
     }
     HIPCHK(hipMemcpyAsync(c->win, hw.data(), hw.size() * 4, hipMemcpyHostToDevice, c->stream));
     std::unique_lock<std::mutex> baton;  // held while this encoder is enqueued (EncBaton)
-    if (c->baton) baton = std::unique_lock<std::mutex>(c->baton->mu);
+    // Encoders of fewer than 9 windows skip the baton: a streaming call's 1-4-window encoder
+    // fills a fraction of the GPU, so sibling lanes' small encoders run side by side
+    // (config 5: 149.0 -> 154.9 calls/s, final-transcript lag p50 5.96 -> 5.44 s; 4 concurrent
+    // 3 s callers 161.6 -> 169.0 calls/s; gpurun_out/r03_ai).  The 64-window batches keep it.
+    // OSW_BATON_MIN_WINDOWS=n: skip below n windows (0: never skip).
+    static const int baton_min = [] {
+        const char* e = std::getenv("OSW_BATON_MIN_WINDOWS");
+        return e ? atoi(e) : 9;
+    }();
+    if (c->baton && n >= baton_min) baton = std::unique_lock<std::mutex>(c->baton->mu);
     // the encoder's kernels go to the low-priority encoder stream (swapped in as c->stream
     // for the launch helpers), fenced by events on both sides
     hipStream_t dec_stream = c->stream;

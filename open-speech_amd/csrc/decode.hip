@@ -1287,7 +1287,11 @@ void launch_dec_self_attn(const float* part, int ks, const float* bias, h16* kc,
         const char* e = std::getenv("OSW_SELF_VPRE");
         return e ? (e[0] == '1' ? 1 : 0) : -1;
     }();
-    const bool vlate = vpre_env < 0 ? B > 8 : vpre_env == 0;
+    static const int vpre_rows = [] {  // OSW_SELF_VPRE_ROWS=n: the row limit of the default
+        const char* e = std::getenv("OSW_SELF_VPRE_ROWS");
+        return e ? atoi(e) : 8;
+    }();
+    const bool vlate = vpre_env < 0 ? B > vpre_rows : vpre_env == 0;
     if (anc) {  // ctx <= 448 (osw.hip checks the context at decode)
         if (vlate)
             dec_self_attn_kernel<true, false><<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, lo_off,

@@ -651,7 +651,8 @@ void encode(osw_ctx* c, const osw_window* wins, int n) {
     std::unique_lock<std::mutex> baton;  // held while this encoder is enqueued (EncBaton)
     // Encoders of fewer than 9 windows skip the baton: a streaming call's 1-4-window encoder
     // fills a fraction of the GPU, so sibling lanes' small encoders run side by side
-    // (config 5: 149.0 -> 154.9 calls/s, final-transcript lag p50 5.96 -> 5.44 s; 4 concurrent
+    // (config 5, one A/B run: 149.0 -> 154.9 calls/s, lag p50 5.96 -> 5.44 s, +2-3 % over every
+    // run on record; 4 concurrent
     // 3 s callers 161.6 -> 169.0 calls/s; gpurun_out/r03_ai).  The 64-window batches keep it.
     // OSW_BATON_MIN_WINDOWS=n: skip below n windows (0: never skip).
     static const int baton_min = [] {

@@ -13,7 +13,9 @@
  *   osw_transcribe_batch
  *       replaces  WhisperModel.transcribe(path, task, beam_size, temperature,
  *                 language, initial_prompt) + list(segments)     (:235-246),
- *                 for the first 30 s window of every clip (greedy, beam_size = 1)
+ *                 for the first 30 s window of every clip; greedy, beam search
+ *                 (beam_size > 1, the reference's default 5) or sampling
+ *                 (temperature > 0, best_of rows), chosen per call by osw_decode_opts
  *   osw_log_mel / osw_encode_windows / osw_decode_windows
  *       the same work split by stage, as faster-whisper's generate_segments seek
  *       loop needs it (FeatureExtractor -> encode -> generate per 30 s window)
@@ -140,6 +142,12 @@ int osw_destroy(osw_ctx* ctx);
  * return OSW_EINVAL. */
 int osw_create_sibling(osw_ctx* parent, int32_t max_batch, osw_ctx** out);
 
+/* Sibling contexts serialise their encoders on the GPU (the encoder baton: one lane
+ * encodes while the others decode); an encoder of fewer than `min_windows` windows skips
+ * it, so small streaming encoders of sibling lanes run side by side.  Default 9
+ * (OSW_BATON_MIN_WINDOWS); 0 = every encoder takes the baton.  Per context. */
+int osw_set_encoder_baton_min(osw_ctx* ctx, int32_t min_windows);
+
 /* Upload one canonical tensor (names and dtypes: open-speech_amd/weights.py). */
 int osw_set_weight(osw_ctx* ctx, const char* name, const void* host, int64_t nbytes);
 /* Read one tensor back as stored on the device (enc.conv1.w: the padded [De][3][C1]
@@ -162,10 +170,15 @@ int osw_get_mel(osw_ctx* ctx, int32_t clip, float* out, int64_t out_floats);  /*
 int osw_encode_windows(osw_ctx* ctx, const osw_window* windows, int32_t n);
 int osw_get_encoder_output(osw_ctx* ctx, int32_t window, float* out, int64_t out_floats); /* [1500][D] */
 
-/* Greedy decode of the n windows last encoded. */
+/* Decode of the n windows last encoded, per `opts`: greedy (beam_size <= 1,
+ * temperature <= 0), CTranslate2-style beam search (beam_size > 1; the reference calls
+ * beam_size = 5, src/backends/faster_whisper.py:237) or sampling (temperature > 0,
+ * best_of rows per window).  The prompt, logits rules and stop rules are the same in
+ * all three modes. */
 int osw_decode_windows(osw_ctx* ctx, int32_t n, const osw_decode_opts* opts, osw_window_result* res);
 
-/* mel + encode + greedy decode of window 0 (seek 0, min(frames, 3000)) of every clip. */
+/* mel + encode + decode (greedy, beam search or sampling per `opts`, as
+ * osw_decode_windows) of window 0 (seek 0, min(frames, 3000)) of every clip. */
 int osw_transcribe_batch(osw_ctx* ctx, const int16_t* pcm, const int64_t* offsets, int32_t n_clips,
                          int32_t pcm_on_device, const osw_decode_opts* opts, osw_window_result* res);
 

@@ -175,6 +175,7 @@ struct osw_ctx {
     bool sibling = false;         // weights belong to another context: read-only here
     bool finalized = false;
     std::shared_ptr<EncBaton> baton;  // shared with sibling contexts; null: encoders not serialised
+    int baton_min = 9;                // encoders of fewer windows skip the baton (osw_set_encoder_baton_min)
     bool share_cus = false;           // this call's encoder GEMMs leave CUs to sibling lanes
     // OSW_ENC_PRIO=1: the encoder runs on its own low-priority stream, the decoder on a
     // high-priority `stream` (measured slower: the default is one stream per lane)
@@ -599,8 +600,15 @@ void run_gemm(osw_ctx* c, const GemmArgs& g0, int cls) {
     g.share_cus = c->share_cus;
     REQUIRE(g.K % 64 == 0, "GEMM K must be a multiple of 64");
     REQUIRE(!g.A_lo || g.epi == EPI_F32, "hi/lo operands feed fp32 outputs only");
+    const bool skinny = skinny_ok(g);
+    // the tiled kernels' non-fp32 epilogues leave through an LDS image in 16-B chunks
+    // (staged_epilogue_sq, the 256-tile staged epilogues) and check only each chunk's
+    // first column against N: every row start must be 16-B aligned and N whole chunks
+    REQUIRE(skinny || g.epi == EPI_F32 ||
+                (g.N % 8 == 0 && (g.epi == EPI_HEADS || (g.ldc % 8 == 0 && g.c_grp_stride % 8 == 0))),
+            "GEMM epilogue needs N, ldc and the C group stride to be multiples of 8");
     Timed t(c, cls, 2.0 * g.M * g.N * g.K);
-    if (skinny_ok(g)) {
+    if (skinny) {
         REQUIRE((int64_t)skinny_ksplit(g.N, g.K) * g.M * g.N <= c->part_floats, "split-K workspace too small");
         launch_gemm_skinny(g, c->part, c->stream);
     } else {
@@ -649,17 +657,13 @@ void encode(osw_ctx* c, const osw_window* wins, int n) {
     }
     HIPCHK(hipMemcpyAsync(c->win, hw.data(), hw.size() * 4, hipMemcpyHostToDevice, c->stream));
     std::unique_lock<std::mutex> baton;  // held while this encoder is enqueued (EncBaton)
-    // Encoders of fewer than 9 windows skip the baton: a streaming call's 1-4-window encoder
-    // fills a fraction of the GPU, so sibling lanes' small encoders run side by side
-    // (config 5, one A/B run: 149.0 -> 154.9 calls/s, lag p50 5.96 -> 5.44 s, +2-3 % over every
-    // run on record; 4 concurrent
-    // 3 s callers 161.6 -> 169.0 calls/s; gpurun_out/r03_ai).  The 64-window batches keep it.
-    // OSW_BATON_MIN_WINDOWS=n: skip below n windows (0: never skip).
-    static const int baton_min = [] {
-        const char* e = std::getenv("OSW_BATON_MIN_WINDOWS");
-        return e ? atoi(e) : 9;
-    }();
-    if (c->baton && n >= baton_min) baton = std::unique_lock<std::mutex>(c->baton->mu);
+    // Encoders of fewer than c->baton_min (9) windows skip the baton: a streaming call's
+    // 1-4-window encoder fills a fraction of the GPU, so sibling lanes' small encoders run
+    // side by side.  Basis: the 4-concurrent-caller probe, 161.6 -> 169.0 calls/s
+    // (gpurun_out/r03_ai); the config-5 simulation moved 149.0 -> 154.9 calls/s in that run,
+    // but it spreads 148.6-156.0 run to run, so its gain is within noise.
+    // The 64-window batches keep the baton.
+    if (c->baton && n >= c->baton_min) baton = std::unique_lock<std::mutex>(c->baton->mu);
     // the encoder's kernels go to the low-priority encoder stream (swapped in as c->stream
     // for the launch helpers), fenced by events on both sides
     hipStream_t dec_stream = c->stream;
@@ -1316,6 +1320,8 @@ int osw_create(const osw_dims* dims, int32_t device, int32_t max_batch, osw_ctx*
         c->R = max_batch * 5;  // room for the reference's beam_size = 5 at full batch
         c->C1 = (dims->n_mels + 63) / 64 * 64;
         if (const char* e = std::getenv("OSW_NO_GRAPH")) c->use_graph = !(e[0] == '1');
+        // OSW_BATON_MIN_WINDOWS=n: encoders below n windows skip the baton (0: never skip)
+        if (const char* e = std::getenv("OSW_BATON_MIN_WINDOWS")) c->baton_min = atoi(e);
         DeviceScope dev_scope_((device));
         make_streams(c);
         const char* eb = std::getenv("OSW_ENC_BATON");
@@ -1352,6 +1358,7 @@ int osw_create_sibling(osw_ctx* parent, int32_t max_batch, osw_ctx** out) {
         c->R = max_batch * 5;
         c->C1 = parent->C1;
         c->use_graph = parent->use_graph;
+        c->baton_min = parent->baton_min;
         DeviceScope dev_scope_((c->device));
         make_streams(c);
         c->w = parent->w;          // same device pointers
@@ -1607,6 +1614,15 @@ int osw_debug_gemm(osw_ctx* c, int32_t M, int32_t N, int32_t K, int32_t variant,
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
         for (void* p : tmp) (void)hipFree(p);
+    });
+}
+
+int osw_set_encoder_baton_min(osw_ctx* c, int32_t min_windows) {
+    return guard([&] {
+        REQUIRE(c, "null ctx");
+        REQUIRE(min_windows >= 0, "min_windows must be >= 0");
+        std::lock_guard<std::mutex> lk(c->mu);
+        c->baton_min = min_windows;
     });
 }
 

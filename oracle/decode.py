@@ -88,6 +88,7 @@ class WindowResult:
     language: int
     step_logits: list = field(default_factory=list)   # raw fp32 logits per generated step
     prompt_logits: list = field(default_factory=list)
+    hypotheses: list = field(default_factory=list)    # beam: every finished (tokens, raw, normalised score), in order
 
 
 def detect_language(raw_sot_logits: np.ndarray, st) -> int:
@@ -178,6 +179,10 @@ class BeamOptions:
     patience: float = 1.0
     length_penalty: float = 1.0
     num_hypotheses: int = 1
+    # the length a finished score is normalised by counts its <|endoftext|> (transformers'
+    # convention, generated_len = cur_len + 1 - prompt_len, generation/utils.py:3182); only
+    # the transformers cross-check sets it (tools/make_hf_pins.py)
+    length_counts_eot: bool = False
 
 
 def _norm_score(score: float, n: int, length_penalty: float) -> float:
@@ -233,7 +238,8 @@ def beam_from_encoder(oracle, xkv, st, *, language=None, task=None, prev_tokens=
                 if k == 0:
                     top_fin = True
                 toks = list(alive[q][0]) + ([] if tok == st.eot else [tok])
-                finished.append((_norm_score(s, len(toks), beam.length_penalty), s, toks))
+                n_len = len(toks) + (1 if beam.length_counts_eot and tok == st.eot else 0)
+                finished.append((_norm_score(s, n_len, beam.length_penalty), s, toks))
                 for j in range(sec, 2 * K):
                     if cands[j][2] != st.eot:
                         nb, sec = j, j + 1
@@ -254,7 +260,8 @@ def beam_from_encoder(oracle, xkv, st, *, language=None, task=None, prev_tokens=
     for f in finished[1:]:
         if f[0] > best[0]:
             best = f
-    return WindowResult(tokens=best[2], sum_logprob=best[1], no_speech_prob=nsp, language=lang)
+    return WindowResult(tokens=best[2], sum_logprob=best[1], no_speech_prob=nsp, language=lang,
+                        hypotheses=[(f[2], f[1], f[0]) for f in finished])
 
 
 # ---------------------------------------------------------------------------

@@ -446,6 +446,10 @@ def test_sibling_encodes_while_lane_captures_graphs(tiny_engine):
     import threading
     d, eng, w = tiny_engine
     sib = eng.sibling(max_batch=2)
+    # 2-window encoders skip the baton by default (baton_min 9): force both lanes to take
+    # it, or neither would record or wait on the event this test is about
+    eng.set_encoder_baton_min(0)
+    sib.set_encoder_baton_min(0)
     try:
         sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
         clips = [synth.chirp_clip(41, 30.0), synth.chirp_clip(42, 9.0)]
@@ -481,4 +485,5 @@ def test_sibling_encodes_while_lane_captures_graphs(tiny_engine):
         for outs, r in zip(got[:2], ref):
             assert [o.tokens for o in outs] == [o.tokens for o in r]
     finally:
+        eng.set_encoder_baton_min(9)
         sib.close()

@@ -72,7 +72,7 @@ EMB_STD = 0.1
 # <|endoftext|> row per case: the plain decode collapses to token 2452, the one under the
 # timestamp rules to 38915
 EOT_MIX = {"plain": ((2452, 0.7), (38915, 0.3)), "rules": ((38915, 0.9), (2452, 0.1))}
-CLIPS = (3, 11)
+CLIPS = (3,)
 MAX_LEN = 60
 BEAM = 5
 

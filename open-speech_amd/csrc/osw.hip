@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <pthread.h>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -253,6 +254,19 @@ struct osw_ctx {
 namespace {
 const int T_ENC = 1500;
 const int N_FR = 3000;
+
+// OSW_TRACE_GRAPH=1: one stderr line per decode-graph event (capture, instantiate, launch,
+// LRU destroy) with the calling thread and context, to correlate host-side crashes of a
+// tool that intercepts HIP (e.g. a profiler) with what the lanes were doing
+void trace_graph(const osw_ctx* c, const char* what) {
+    static const bool on = [] {
+        const char* e = std::getenv("OSW_TRACE_GRAPH");
+        return e && e[0] == '1';
+    }();
+    if (!on) return;
+    std::fprintf(stderr, "[osw-graph] thread %zx ctx %p %s\n", (size_t)pthread_self(), (const void*)c, what);
+    std::fflush(stderr);
+}
 
 hipEvent_t get_ev(osw_ctx* c) {
     if (!c->ev_free.empty()) {
@@ -997,6 +1011,7 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
                 for (auto it = c->dgraphs.begin(); it != c->dgraphs.end(); ++it)
                     if (it->second.second < lru->second.second) lru = it;
                 HIPCHK(hipStreamSynchronize(c->stream));
+                trace_graph(c, "destroy (LRU)");
                 HIPCHK(hipGraphExecDestroy(lru->second.first));
                 c->dgraphs.erase(lru);
             }
@@ -1011,9 +1026,11 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
             if (c->baton) no_encoder = std::unique_lock<std::mutex>(c->baton->mu);
             c->capturing = true;
             try {
+                trace_graph(c, "capture begin");
                 HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
                 for (int i = 0; i < CH; ++i) one_step();
                 HIPCHK(hipStreamEndCapture(c->stream, &gr));
+                trace_graph(c, "capture end");
             } catch (...) {
                 c->capturing = false;
                 hipGraph_t junk = nullptr;
@@ -1023,6 +1040,7 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
             }
             c->capturing = false;
             hipError_t e = hipGraphInstantiate(&c->dgraph, gr, nullptr, nullptr, 0);
+            trace_graph(c, "instantiated");
             (void)hipGraphDestroy(gr);
             HIPCHK(e);
             c->dgraphs[key] = {c->dgraph, ++c->dgraph_tick};
@@ -1035,6 +1053,7 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
         while (steps < max_len) {
             int did;
             if (graph && max_len - steps >= CH) {
+                trace_graph(c, "launch");
                 HIPCHK(hipGraphLaunch(c->dgraph, c->stream));
                 did = CH;
             } else {

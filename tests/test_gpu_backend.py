@@ -1,5 +1,6 @@
 """End-to-end through the drop-in backend on the GPU (real engine, random weights)."""
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -163,3 +164,112 @@ def test_backend_verbose_json_matches_oracle_seek_loop(monkeypatch, tmp_path, va
         wt = tok.decode(gpu[(s["seek"], next(z for sk, z in gpu if sk == s["seek"]))][1].tokens).strip().encode()
         assert s["compression_ratio"] == (len(wt) / len(zlib.compress(wt)) if wt else 0.0)
     assert r["text"] == "".join(s["text"] for s in r["segments"]).strip()
+
+
+def test_backend_default_config_matches_oracle_seek_loop(monkeypatch, tmp_path):
+    """The backend as deployed: its defaults (STT_HIP_BEAM_SIZE 5 = the reference's
+    beam_size, src/backends/faster_whisper.py:237; 3 lanes per GPU; max batch 16; the
+    batcher's 1 ms gap), three concurrent requests (75, 61 and 47 s WAVs) so the batcher
+    spreads windows over the lanes and batches windows of different clips.  Every lane is
+    recorded; each request's windows are replayed through the oracle's seek loop with the
+    oracle's CTranslate2-BeamSearch restatement (width 5) decoding the GPU's own encoder
+    output: every prompt and every window's ids must equal the oracle's, and each response's
+    segments the oracle's.  Model: micro dims with the synthetic tokenizer (tests/tokfix.py),
+    so the numpy beam oracle stays fast over full 448-position windows."""
+    import hashlib
+
+    import tokfix
+    from oracle import decode as odec
+    from oracle import seek as oseek
+    from oracle.model import WhisperOracle
+    from open_speech_amd import dims as D
+    from open_speech_amd import model_store
+    from open_speech_amd.engine import WhisperEngine
+    from open_speech_amd.tokenizer import WhisperTokenizer, get_suppressed_tokens
+
+    for k in ("STT_HIP_BEAM_SIZE", "STT_HIP_LANES", "STT_HIP_MAX_BATCH", "STT_HIP_BATCH_GAP_MS",
+              "STT_HIP_BATCH_WAIT_MS", "STT_HIP_TOKENS_PER_SEC"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("STT_HIP_GPUS", "0")
+
+    calls = []              # (clip hash, seek, size, prompt, output, encoder output) over every lane
+    lock = threading.Lock()
+
+    class Recorder:
+        def __init__(self, eng):
+            self.eng, self._clips, self._wins = eng, [], []
+
+        def __getattr__(self, k):
+            return getattr(self.eng, k)
+
+        def sibling(self, max_batch=None):
+            return Recorder(self.eng.sibling(max_batch))
+
+        def log_mel(self, clips, *a, **kw):
+            self._clips = [hashlib.sha1(np.asarray(c, np.int16).tobytes()).hexdigest() for c in clips]
+            return self.eng.log_mel(clips, *a, **kw)
+
+        def encode(self, wins):
+            self._wins = list(wins)
+            self.eng.encode(wins)
+            self._enc = [self.eng.encoder_output(k) for k in range(len(wins))]
+
+        def decode(self, n, cfg, prefix=None, dump_steps=0, languages=None):
+            assert cfg.beam_size == 5, "the backend's default decoding is beam search width 5"
+            outs = self.eng.decode(n, cfg, prefix=prefix, languages=languages)
+            with lock:
+                for k, (c, seek, size) in enumerate(self._wins):
+                    calls.append((self._clips[c], seek, size, list(prefix[k]) if prefix else [], outs[k],
+                                  self._enc[k]))
+            return outs
+
+    def factory(dims, gpu, max_batch):
+        return Recorder(WhisperEngine(dims, device=gpu, max_batch=max_batch))
+
+    mid = tokfix.make_hf_model_dir(str(tmp_path / "micro_hf"), D.MICRO_TEST)
+    b = HipWhisperBackend(engine_factory=factory)
+    b.load_model(mid)
+    clips = [synth.chirp_clip(51 + i, s) for i, s in enumerate((75.0, 61.0, 47.0))]
+    res = [None] * len(clips)
+    try:
+        def go(i):
+            res[i] = b.transcribe(synth.to_wav_bytes(clips[i]), mid, response_format="verbose_json")
+        engines = list(b._models[mid].engines)
+        ts = [threading.Thread(target=go, args=(i,)) for i in range(len(clips))]
+        for t in ts:
+            t.start()
+            time.sleep(0.05)    # later requests arrive while the first lane is busy: other lanes take them
+        for t in ts:
+            t.join(timeout=600)
+    finally:
+        b.unload_model(mid)
+    assert len(engines) == 3 and all(r is not None for r in res)
+    src = model_store.resolve(mid)
+    d, w = src.dims, model_store.load_weights(src)
+    tok = WhisperTokenizer(d.n_vocab, src.tokenizer_json)
+    st = tok.special
+    sup = get_suppressed_tokens(tok, [-1])
+    orc = WhisperOracle(d, w, fp16=True)
+    by_key = {}
+    for h, seek, size, p, o, enc in calls:
+        by_key.setdefault((h, seek, size), []).append((p, o, enc))
+    for pcm, r in zip(clips, res):
+        h = hashlib.sha1(pcm.tobytes()).hexdigest()
+        lang = {}
+
+        def decode_window(seek, size, prompt_toks):
+            (gp, go, enc), = by_key[(h, seek, size)]
+            o = odec.beam_from_encoder(orc, orc.cross_kv(enc), st, language=lang.get("tok"),
+                                       prev_tokens=prompt_toks[1:], opts=odec.DecodeOptions(suppress_tokens=sup),
+                                       beam=odec.BeamOptions(beam_size=5))
+            lang.setdefault("tok", o.language)
+            assert gp == prompt_toks, f"{len(pcm)} samples, window {seek}: prompt differs"
+            assert go.tokens == o.tokens, f"{len(pcm)} samples, window {seek}: ids differ from the oracle's"
+            return go.tokens, go.sum_logprob, go.no_speech_prob
+
+        wins = oseek.seek_loop(decode_window, (len(pcm) + 160) // 160, st, tok.decode)
+        want = [(round(a, 6), round(e, 6), t) for x in wins for a, e, t in x.segments]
+        got = [(round(s["start"], 6), round(s["end"], 6), s["tokens"]) for s in r["segments"]]
+        assert got == want
+    # the three requests' windows went through more than one lane
+    assert sum(1 for e in engines if e._wins) >= 2

@@ -19,17 +19,24 @@ pytestmark = pytest.mark.gpu
 MID = "random:large-v3-turbo"
 
 
-def test_streaming_sessions_equal_cold_single_calls(monkeypatch):
+@pytest.mark.parametrize("sessions,speech_s,max_batch", [(8, 2.0, "8"), (32, 6.0, None)])
+def test_streaming_sessions_equal_cold_single_calls(monkeypatch, sessions, speech_s, max_batch):
+    """(8, 2 s, max batch 8): a quick form.  (32, 6 s, backend defaults): BASELINE
+    configs[4] at its stated size, ~2000 calls, every one re-checked cold."""
     import bench
     monkeypatch.setenv("STT_HIP_TOKENS_PER_SEC", "4")    # random weights never emit <|endoftext|>
-    monkeypatch.setenv("STT_HIP_MAX_BATCH", "8")
+    if max_batch:
+        monkeypatch.setenv("STT_HIP_MAX_BATCH", max_batch)
+    else:
+        monkeypatch.delenv("STT_HIP_MAX_BATCH", raising=False)
     monkeypatch.setenv("STT_HIP_GPUS", "0")
     be = HipWhisperBackend()
     try:
         rec = []
-        stats = bench.stream_sessions(8, 2.0, model=MID, backend=be, record=rec)
-        assert stats["transcriptions"] == len(rec) > 8
-        assert {i for i, _, _ in rec} == set(range(8))            # every session was served
+        stats = bench.stream_sessions(sessions, speech_s, model=MID, backend=be, record=rec)
+        print("streaming", sessions, "sessions:", stats)
+        assert stats["transcriptions"] == len(rec) > sessions
+        assert {i for i, _, _ in rec} == set(range(sessions))     # every session was served
         assert stats["final_transcript_lag_p50_s"] is not None
         # the reference's beam_size 5 (backend default), same bytes, nothing else in flight
         for i, wav, got in rec:

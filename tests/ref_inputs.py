@@ -11,7 +11,7 @@ import wave
 
 import numpy as np
 
-from .synth import chirp_clip, to_wav_bytes
+from open_speech_amd.synth import chirp_clip, to_wav_bytes
 
 
 def _wav(pcm: np.ndarray, sr: int, ch: int = 1, width: int = 2) -> bytes:

@@ -15,7 +15,8 @@ from types import SimpleNamespace
 import numpy as np
 import pytest
 
-from open_speech_amd import ref_inputs, segments
+import ref_inputs
+from open_speech_amd import segments
 from oracle import ingest as oi
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")

@@ -11,7 +11,8 @@ import os
 import numpy as np
 import pytest
 
-from open_speech_amd import ingest, ref_inputs
+import ref_inputs
+from open_speech_amd import ingest
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")

@@ -12,6 +12,7 @@ typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short s16x4 __attribute__((vector_size(8)));
 
 #define OSW_LDS __attribute__((address_space(3)))
@@ -135,6 +136,9 @@ struct GemmArgs {
     // MFMA B fragment of one k32 step is 1 KB contiguous, so a wave's weight load is one
     // coalesced 1-KB piece instead of 16 rows x 64 B; launch_frag_pack), or nullptr
     const h16* Wf;
+    // skinny kernel: A of the 64-column block bx starts at A + bx * a_col_stride (the V
+    // projection of the E-form cross-attention: one head's normalised P·E per block)
+    int64_t a_col_stride;
 };
 
 // fp32 -> (hi, lo) fp16 pair: hi = fp16(v), lo = fp16(v - hi)

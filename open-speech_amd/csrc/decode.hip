@@ -779,6 +779,23 @@ __global__ __launch_bounds__(256) void dec_reduce_gelu_kernel(const float* __res
         split_h16(gelu_reduce_one(part, ks, total, bias, i, (int)(i % N)), y, y + lo_off, i);
 }
 
+// the E-form V projection's split-K reduce: y = bias + Σ_k part[k] (k in order) as an hi/lo pair
+__global__ __launch_bounds__(256) void dec_reduce_kernel(const float* __restrict__ part, int ks, int64_t total, int N,
+                                                         const float* __restrict__ bias, h16* __restrict__ y,
+                                                         int64_t lo_off) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        float p[8];
+        float v = 0.f;
+        for (int k0 = 0; k0 < ks; k0 += 8) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) p[j] = part[(int64_t)min(k0 + j, ks - 1) * total + i];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v += k0 + j < ks ? p[j] : 0.f;
+        }
+        split_h16(bias[(int)(i % N)] + v, y, y + lo_off, i);
+    }
+}
+
 #include "select.h"
 
 // ---------------------------------------------------------------------------
@@ -1345,6 +1362,13 @@ void launch_dec_resid_ln(const float* part, int ks, int B, int D, const float* b
                          const int* tok, const int* pos, int ctx, int V, hipStream_t s) {
     ResLnArgs A{part, ks, (int64_t)B * D, bias, x, x, g, be, tok_emb, pos_emb, tok, pos, ctx, D, V};
     dec_resid_ln_kernel<<<B, 256, 0, s>>>(A, y, lo_off);
+}
+
+void launch_dec_reduce(const float* part, int ks, int B, int N, const float* bias, h16* y, int64_t lo_off,
+                       hipStream_t s) {
+    const int64_t total = (int64_t)B * N;
+    dec_reduce_kernel<<<(unsigned)std::min<int64_t>((total + 255) / 256, 1024), 256, 0, s>>>(part, ks, total, N, bias,
+                                                                                            y, lo_off);
 }
 
 void launch_dec_reduce_gelu(const float* part, int ks, int B, int N, const float* bias, h16* y, int64_t lo_off,

@@ -1,0 +1,12 @@
+# round-4 call: exattn probe + the E-form GPU tests + headline A/B
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r04_f; mkdir -p $O
+set -e
+timeout -k 10 120 ./tools/probe/exattn_probe 64 > $O/probe.txt 2>&1; cat $O/probe.txt
+OSW_EFORM=1 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+  tests/test_gpu_parity.py tests/test_gpu_robustness.py tests/test_gpu_turbo.py > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+A="--steps 10 --latency-repeats 0 --beam5-latency-repeats 0 --beam5 0 --realistic-steps 0 --no-cpu-baseline --stream-sessions 0"
+OSW_EFORM=1 timeout -k 10 300 python -u bench.py $A > $O/eform.json 2> $O/eform.err
+OSW_EFORM=0 timeout -k 10 300 python -u bench.py $A > $O/noeform.json 2> $O/noeform.err
+for f in eform noeform; do python3 -c "import json;d=json.load(open('$O/$f.json'));print('$f',d['value'],d['ms_per_step'],d['tokens_per_clip'])"; done

@@ -24,6 +24,9 @@ MID = "random:large-v3-turbo"
 os.environ.setdefault("STT_HIP_TOKENS_PER_SEC", "4")
 be = HipWhisperBackend()
 be.load_model(MID)
+if os.environ.get("STREAM_PROBE_MAPS"):   # shared-object map, to attribute a native crash's frames
+    with open("/proc/self/maps") as src, open(os.environ["STREAM_PROBE_MAPS"], "w") as dst:
+        dst.write(src.read())
 wavs = {s: pcm_to_wav(synth.chirp_clip(500, s).tobytes(), 16000) for s in (1.0, 3.0, 6.0)}
 
 

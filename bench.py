@@ -67,7 +67,9 @@ def parse(argv=None):
                     help="BASELINE configs[4]: concurrent /v1/audio/stream sessions simulated through the backend "
                          "(0 = skip)")
     ap.add_argument("--stream-speech-s", type=float, default=6.0, help="seconds of speech per streaming session")
-    ap.add_argument("--realistic-steps", type=int, default=6,
+    ap.add_argument("--refill-min", type=int, default=8,
+                    help="row refill (realistic lengths): admit queued clips once this many rows are free")
+    ap.add_argument("--realistic-steps", type=int, default=9,
                     help="also time this many steps with realistic output lengths (random weights never emit "
                          "<|endoftext|>: each clip's length is forced from a seeded distribution)")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r03_fin3_pmc.json"),
@@ -307,7 +309,7 @@ def ingest_timing(repeats: int = 30, device: int = 0) -> dict:
             "repeats": repeats, "note": "bytes in, bytes out; host = the reference's numpy/scipy ops, one thread"}
 
 
-def timed_steps(dp, allpcm, k: int, dist=None, dev=None):
+def timed_steps(dp, allpcm, k: int, dist=None, dev=None, runner=None):
     """The bench contract's timed region: barrier + device sync on both sides of exactly
     k steps, then the MAX of the elapsed time over ranks and the SUM of tokens decoded.
     Returns (seconds, total tokens over all ranks, per-step results of this rank)."""
@@ -321,7 +323,7 @@ def timed_steps(dp, allpcm, k: int, dist=None, dev=None):
         dist.barrier()
     sync()
     t0 = time.perf_counter()
-    res = dp.run_steps(allpcm, k)
+    res = (runner or dp.run_steps)(allpcm, k)
     sync()
     if dist:
         dist.barrier()
@@ -410,20 +412,30 @@ def main(argv=None):
     # Realistic output lengths: real speech gives ~2-6 tokens per second of audio (text +
     # timestamp pairs), so each clip's greedy decode is cut at a length drawn from
     # N(130, 40) clipped to [16, 440] (seeded; the same lengths on every rank) by the
-    # decoder's token budget.  Finished rows skip their self / cross-attention, so a
-    # batch's cost follows its clips' lengths, not the longest one's worst case.
+    # decoder's token budget.  Finished rows skip their self / cross-attention; with row
+    # refill (the default, WhisperEngine.transcribe_refill) a finished window's row takes
+    # the next queued clip, so a lane's rows stay full across its steps instead of every
+    # batch waiting for its longest window.  The plain per-batch path is timed beside it.
     realistic = None
     if a.realistic_steps > 0:
         lens = np.clip(np.round(np.random.default_rng(77).normal(130, 40, B)), 16, 440).astype(int)
         import dataclasses
         dp.cfg = dataclasses.replace(cfg, token_budget=tuple(int(x) for x in lens))
         dp.run_steps(allpcm, len(dp.lanes))
-        rel, rtok_all, _ = timed_steps(dp, allpcm, a.realistic_steps, dist, dev)
+        rel0, rtok0, _ = timed_steps(dp, allpcm, a.realistic_steps, dist, dev)
+        refill = lambda pcm, k: dp.run_steps_refill(pcm, k, refill_min=a.refill_min)  # noqa: E731
+        refill(allpcm, len(dp.lanes))  # every lane captures its refill graph
+        rel, rtok_all, _ = timed_steps(dp, allpcm, a.realistic_steps, dist, dev, runner=refill)
         rtok = rtok_all / (n_total * a.realistic_steps)
         realistic = {"value": round(n_total * a.realistic_steps * 30.0 / rel, 2), "unit": "audio-sec/sec",
                      "steps": a.realistic_steps, "ms_per_step": round(rel / a.realistic_steps * 1e3, 2),
                      "tokens_per_clip": round(rtok, 1), "max_tokens_per_clip": int(lens.max()),
-                     "lengths": "N(130, 40) clipped to [16, 440], seed 77"}
+                     "lengths": "N(130, 40) clipped to [16, 440], seed 77",
+                     "row_refill": {"refill_min": a.refill_min,
+                                    "steps_per_lane_call": -(-a.realistic_steps // len(dp.lanes))},
+                     "no_refill": {"value": round(n_total * a.realistic_steps * 30.0 / rel0, 2),
+                                   "ms_per_step": round(rel0 / a.realistic_steps * 1e3, 2),
+                                   "tokens_per_clip": round(rtok0 / (n_total * a.realistic_steps), 1)}}
         dp.cfg = cfg
 
     # The reference's own decoding (beam_size=5, src/backends/faster_whisper.py:237) on the

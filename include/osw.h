@@ -188,6 +188,17 @@ int osw_decode_windows(osw_ctx* ctx, int32_t n, const osw_decode_opts* opts, osw
 int osw_transcribe_batch(osw_ctx* ctx, const int16_t* pcm, const int64_t* offsets, int32_t n_clips,
                          int32_t pcm_on_device, const osw_decode_opts* opts, osw_window_result* res);
 
+/* Greedy transcription of window 0 of every clip (as osw_transcribe_batch) with row refill:
+ * the decoder keeps max_batch rows, each with its own step counter, and a finished
+ * window's row is refilled with the next queued clip (its window encoded straight into
+ * that row's cross-K/V slot) once refill_min rows are free.  n_clips may exceed max_batch.
+ * Each clip's result equals osw_transcribe_batch's.  Replaces the same per-file
+ * WhisperModel.transcribe calls (src/backends/faster_whisper.py:235-246) when a caller has
+ * many files queued; opts: temperature 0, beam_size 1, no prefix (OSW_EINVAL otherwise). */
+int osw_transcribe_refill(osw_ctx* ctx, const int16_t* pcm, const int64_t* offsets, int32_t n_clips,
+                          int32_t pcm_on_device, const osw_decode_opts* opts, osw_window_result* res,
+                          int32_t refill_min);
+
 /* Parity helper: one encoder block on x [T][D] fp32 (host), result to y (host). */
 int osw_encoder_layer_debug(osw_ctx* ctx, int32_t layer, const float* x, float* y, int32_t T);
 

@@ -77,6 +77,8 @@ _SIGS = {
     "osw_decode_windows": (C.c_int, [C.c_void_p, C.c_int32, P(osw_decode_opts), P(osw_window_result)]),
     "osw_transcribe_batch": (C.c_int, [C.c_void_p, C.c_void_p, P(C.c_int64), C.c_int32, C.c_int32,
                                        P(osw_decode_opts), P(osw_window_result)]),
+    "osw_transcribe_refill": (C.c_int, [C.c_void_p, C.c_void_p, P(C.c_int64), C.c_int32, C.c_int32,
+                                        P(osw_decode_opts), P(osw_window_result), C.c_int32]),
     "osw_encoder_layer_debug": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_float), P(C.c_float), C.c_int32]),
     "osw_debug_gemm": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
                                  P(C.c_float), C.c_int32, P(C.c_float)]),

@@ -114,6 +114,7 @@ struct GemmArgs {
     const float* pos;                    // EPI_F32_GELU_POS: pos[(m % c_grp_rows)][n]
     int epi;
     int heads_T, heads_H, heads_nb;      // EPI_HEADS geometry
+    const int* heads_slot;               // EPI_HEADS: window b of this GEMM goes to slot heads_slot[b] (nullptr: b)
     int band;                            // 256-tile walk: column band width (0 = all columns)
     int kc;                              // 128-tile split-K: K per blockIdx.z, EPI_F32 slab z at C + z*M*ldc (0 = K)
     // decoder activations as an fp16 pair a = hi + lo (hi = fp16(a), lo = fp16(a - hi)):

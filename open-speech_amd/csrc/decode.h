@@ -26,6 +26,7 @@ struct SelParams {
                                      // seed per call replays the captured decode graph)
     const int* budget;     // per decoder row: force <|endoftext|> after this many sampled tokens (<= 0: none);
                            // nullptr: no budgets (osw_decode_opts::token_budget, length-controlled benches)
+    int pos_row;           // 1: row r's step counter is pos[r] (row refill, greedy), 0: one shared counter
 };
 
 // Per window in beam mode: finished-hypothesis bookkeeping (the best one's tokens
@@ -70,6 +71,8 @@ void launch_ex_qk(const float* part, int ks, const float* bias, int rows, int D,
 void launch_exattn(const h16* E, const h16* qp, int64_t qlo, int W, int T, int D, float* ws, int pstride, h16* pen,
                    int64_t pen_lo, const SelState* st, hipStream_t s);
 
+void launch_refill_rows(const int* pack, int k, int P, int* prompt, int* budget, int* cur_tok, int* pos, SelState* st,
+                        hipStream_t s);
 void launch_select(const float* logits, int rows, int* pos, const SelParams& P, const int* prompt,
                    const unsigned* supmask, SelState* st, int* cur_tok, int* tokens, int max_tokens, void* sel_parts,
                    int* arrive, bool bump, void* cand, hipStream_t s);

@@ -217,7 +217,7 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
                                                             h16* __restrict__ vcache, const int* __restrict__ pos_ptr,
                                                             int H, int B, int ctx, h16* __restrict__ out,
                                                             int64_t lo_off, const int* __restrict__ anc, int group,
-                                                            const SelState* __restrict__ st) {
+                                                            const SelState* __restrict__ st, int pos_row) {
     __shared__ h16 q16[HD];
     int h, b;
     if constexpr (GATHER) {
@@ -237,7 +237,8 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
     // the whole batch is done) reads and writes nothing: its outputs are never used
     if (st[b].done) return;
     const int D = H * HD;
-    const int pos = min(*pos_ptr, ctx - 1);  // graph replays may run past max_length on finished windows
+    // graph replays may run past max_length on finished windows; pos_row: per-row counters (row refill)
+    const int pos = min(pos_ptr[pos_row ? b : 0], ctx - 1);
     h16* kc = kcache + ((int64_t)b * H + h) * ctx * HD;
     h16* vc = vcache + ((int64_t)b * H + h) * ctx * HD;
     __shared__ int soff[GATHER ? 512 : 1];
@@ -1019,7 +1020,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void s
                                                      int* __restrict__ tokens, int max_tokens,
                                                      int* __restrict__ arrive, int* __restrict__ ticket, int bump,
                                                      BeamCand* __restrict__ cand) {
-    const int step = *pos_ptr;
+    const int step = pos_ptr[P.pos_row ? blockIdx.x : 0];
     if ((MODE == 2 || MODE == 3) && P.beam > 1) {
         const SelState s = st[blockIdx.x];
         if (sel_mode(P, step, s) == SEL_SAMPLE) {  // the same for every slice of the row
@@ -1048,6 +1049,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void s
     if (threadIdx.x != 0) return;
     select_final_row(logits, P, step, prompt, rp, st, cur_tok, tokens, max_tokens);
     if (!bump) return;
+    if (P.pos_row) {  // row refill: every slice of this row has read its own counter
+        __builtin_amdgcn_s_waitcnt(0);
+        __hip_atomic_store(pos_ptr + b, step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     __builtin_amdgcn_s_waitcnt(0);
     if (__hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
         __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1280,6 +1286,22 @@ __global__ __launch_bounds__(256) void beam_update_kernel(SelParams P, int* __re
     }
 }
 
+// Row refill (osw.hip decode_refill): reset the decoder rows of newly admitted windows.
+// pack[i] = {row, token budget, prompt[0 .. P)}; one workgroup per admitted window.
+__global__ __launch_bounds__(64) void refill_rows_kernel(const int* __restrict__ pack, int P, int* __restrict__ prompt,
+                                                         int* __restrict__ budget, int* __restrict__ cur_tok,
+                                                         int* __restrict__ pos, SelState* __restrict__ st) {
+    const int* e = pack + (int64_t)blockIdx.x * (2 + P);
+    const int row = e[0];
+    for (int j = threadIdx.x; j < P; j += blockDim.x) prompt[(int64_t)row * P + j] = e[2 + j];
+    if (threadIdx.x == 0) {
+        if (budget) budget[row] = e[1];
+        cur_tok[row] = e[2];
+        pos[row] = 0;
+        st[row] = SelState{};
+    }
+}
+
 __global__ void count_done_kernel(const SelState* st, int B, int* out) {
     int c = 0;
     for (int i = threadIdx.x; i < B; i += blockDim.x) c += st[i].done;
@@ -1289,13 +1311,18 @@ __global__ void count_done_kernel(const SelState* st, int B, int* out) {
 
 }  // namespace
 
+void launch_refill_rows(const int* pack, int k, int P, int* prompt, int* budget, int* cur_tok, int* pos, SelState* st,
+                        hipStream_t s) {
+    refill_rows_kernel<<<k, 64, 0, s>>>(pack, P, prompt, budget, cur_tok, pos, st);
+}
+
 int sel_parts_bytes() { return (int)sizeof(SelPart) * SEL_SPLIT; }
 int sel_fused_parts_bytes(int V) { return (int)sizeof(SelPart) * ((V + 63) / 64); }
 int beam_cand_bytes(int) { return (int)sizeof(BeamCand) * BEAM_SLICES * 2 * MAXK2; }
 
 void launch_dec_self_attn(const float* part, int ks, const float* bias, h16* kc, h16* vc, const int* pos, int B,
                           int H, int ctx, h16* out, int64_t lo_off, const int* anc, int group, const SelState* st,
-                          hipStream_t s) {
+                          hipStream_t s, int pos_row) {
     // V issued with K (VPRE, 139 VGPRs) only for a few rows: batch-1 p50 114.3 / 114.8 ->
     // 113.6 / 113.4 ms greedy, 152.2 / 153.5 -> 151.6 / 151.4 ms beam 5; at 64 rows its 3
     // waves per SIMD lose to the 7 of the 66-VGPR form (16.9 -> 20.8 us per launch, beam rows
@@ -1312,16 +1339,16 @@ void launch_dec_self_attn(const float* part, int ks, const float* bias, h16* kc,
     if (anc) {  // ctx <= 448 (osw.hip checks the context at decode)
         if (vlate)
             dec_self_attn_kernel<true, false><<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, lo_off,
-                                                                    anc, group, st);
+                                                                    anc, group, st, pos_row);
         else
             dec_self_attn_kernel<true, true><<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, lo_off,
-                                                                   anc, group, st);
+                                                                   anc, group, st, pos_row);
     } else if (vlate) {
         dec_self_attn_kernel<false, false><<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, lo_off,
-                                                                 nullptr, 1, st);
+                                                                 nullptr, 1, st, pos_row);
     } else {
         dec_self_attn_kernel<false, true><<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, lo_off,
-                                                                nullptr, 1, st);
+                                                                nullptr, 1, st, pos_row);
     }
 }
 
@@ -1359,8 +1386,8 @@ void launch_dec_cross_attn(const float* part, int ks, const float* bias, const h
 
 void launch_dec_resid_ln(const float* part, int ks, int B, int D, const float* bias, float* x, const float* g,
                          const float* be, h16* y, int64_t lo_off, const h16* tok_emb, const float* pos_emb,
-                         const int* tok, const int* pos, int ctx, int V, hipStream_t s) {
-    ResLnArgs A{part, ks, (int64_t)B * D, bias, x, x, g, be, tok_emb, pos_emb, tok, pos, ctx, D, V};
+                         const int* tok, const int* pos, int ctx, int V, hipStream_t s, int pos_row) {
+    ResLnArgs A{part, ks, (int64_t)B * D, bias, x, x, g, be, tok_emb, pos_emb, tok, pos, ctx, D, V, pos_row};
     dec_resid_ln_kernel<<<B, 256, 0, s>>>(A, y, lo_off);
 }
 

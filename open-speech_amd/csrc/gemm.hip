@@ -27,6 +27,10 @@ namespace {
 
 constexpr int BM = 128, BN = 128, BK = 64, NTHR = 256;
 
+// EPI_HEADS: the cross-K/V slot of window b of this GEMM (row refill encodes new windows
+// into the slots of finished ones)
+__device__ __forceinline__ int heads_window(const GemmArgs& g, int b) { return g.heads_slot ? g.heads_slot[b] : b; }
+
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
 __device__ __forceinline__ const h16* grp_row(const h16* base, int64_t m, int64_t grp_rows, int64_t grp_stride,
@@ -54,7 +58,7 @@ __device__ __forceinline__ void store_one(const GemmArgs& g, int m, int n, float
     } else {  // EPI_HEADS: n = which*D + h*64 + d ; m = b*T + t
         const int D = g.heads_H * 64;
         const int which = n / D, h = (n % D) >> 6, d = n & 63;
-        const int b = m / g.heads_T, t = m % g.heads_T;
+        const int b = heads_window(g, m / g.heads_T), t = m % g.heads_T;
         h16* C = (h16*)g.C;
         C[((((int64_t)which * g.heads_nb + b) * g.heads_H + h) * g.heads_T + t) * 64 + d] = (h16)v;
     }
@@ -103,7 +107,7 @@ __device__ __forceinline__ void staged_epilogue_sq(const GemmArgs& g, const f32x
             if constexpr (EPI == EPI_HEADS) {
                 const int D = g.heads_H * 64;
                 const int which = n / D, h = (n % D) >> 6, d = n & 63;
-                const int b = m / g.heads_T, t = m % g.heads_T;
+                const int b = heads_window(g, m / g.heads_T), t = m % g.heads_T;
                 dst = (h16*)g.C + ((((int64_t)which * g.heads_nb + b) * g.heads_H + h) * g.heads_T + t) * 64 + d;
             } else {
                 dst = (h16*)g.C + (m / g.c_grp_rows) * g.c_grp_stride + (int64_t)(m % g.c_grp_rows) * g.ldc + n;
@@ -335,7 +339,7 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
             if constexpr (EPI == EPI_HEADS) {
                 const int D = g.heads_H * 64;
                 const int which = n / D, h = (n % D) >> 6, d = n & 63;
-                const int b = m / g.heads_T, t = m % g.heads_T;
+                const int b = heads_window(g, m / g.heads_T), t = m % g.heads_T;
                 dst = (h16*)g.C + ((((int64_t)which * g.heads_nb + b) * g.heads_H + h) * g.heads_T + t) * 64 + d;
             } else {
                 dst = (h16*)g.C + (m / g.c_grp_rows) * g.c_grp_stride + (int64_t)(m % g.c_grp_rows) * g.ldc + n;
@@ -578,7 +582,7 @@ __device__ __forceinline__ void staged_epilogue_next0(const GemmArgs& g, f32x4 (
                 if constexpr (EPI == EPI_HEADS) {
                     const int D = g.heads_H * 64;
                     const int which = n / D, h = (n % D) >> 6, d = n & 63;
-                    const int b = m / g.heads_T, t = m % g.heads_T;
+                    const int b = heads_window(g, m / g.heads_T), t = m % g.heads_T;
                     dst = (h16*)g.C + ((((int64_t)which * g.heads_nb + b) * g.heads_H + h) * g.heads_T + t) * 64 + d;
                 } else {
                     dst = (h16*)g.C + (m / g.c_grp_rows) * g.c_grp_stride + (int64_t)(m % g.c_grp_rows) * g.ldc + n;

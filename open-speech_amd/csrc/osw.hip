@@ -14,6 +14,7 @@
 #include <cstring>
 #include <map>
 #include <pthread.h>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -36,11 +37,11 @@ void launch_enc_attn(const h16*, h16*, int, int, int, hipStream_t);
 void launch_init_uniform(void*, bool, int64_t, uint64_t, float, float, int64_t, int64_t, hipStream_t);
 uint64_t hash_stream_key(uint64_t, int64_t);
 void launch_dec_self_attn(const float*, int, const float*, h16*, h16*, const int*, int, int, int, h16*, int64_t,
-                          const int*, int, const SelState*, hipStream_t);
+                          const int*, int, const SelState*, hipStream_t, int pos_row = 0);
 void launch_dec_cross_attn(const float*, int, const float*, const h16*, const h16*, int, int, int, int, h16*, int64_t,
                            float*, int*, const SelState*, hipStream_t);
 void launch_dec_resid_ln(const float*, int, int, int, const float*, float*, const float*, const float*, h16*, int64_t,
-                         const h16*, const float*, const int*, const int*, int, int, hipStream_t);
+                         const h16*, const float*, const int*, const int*, int, int, hipStream_t, int pos_row = 0);
 void launch_dec_reduce_gelu(const float*, int, int, int, const float*, h16*, int64_t, hipStream_t);
 void launch_dec_reduce(const float*, int, int, int, const float*, h16*, int64_t, hipStream_t);
 void launch_ingest_sumsq(const int16_t*, int, int, const int2*, int, float*, float*, hipStream_t);
@@ -209,6 +210,9 @@ struct osw_ctx {
         *XKV = nullptr;
     float* X = nullptr;
     int n_encoded = 0;
+    bool row_pos = false;             // decode_refill: per-row step counters (pos[row])
+    int* slot_d = nullptr;            // encode into slots: window -> decoder row
+    int* refill_pack = nullptr;       // decode_refill: rows to admit {row, budget, prompt}
 
     // decoder workspace.  xdn / dattn / dh (the GEMM operands) are hi/lo fp16 pairs:
     // the lo halves sit R rows after the hi halves (lo_off below)
@@ -559,7 +563,9 @@ void setup_workspace(osw_ctx* c) {
     c->vc = dalloc<h16>(kvn, o);
     c->logits = dalloc<float>(R * d.n_vocab, o);
     c->cur_tok = dalloc<int>(R, o);
-    c->pos = dalloc<int>(1, o);
+    c->pos = dalloc<int>(R, o);  // [0]: the shared step counter; [row] in decode_refill
+    c->slot_d = dalloc<int>(B, o);
+    c->refill_pack = dalloc<int>(B * (2 + d.n_text_ctx), o);
     c->tokens = dalloc<int>(R * d.n_text_ctx, o);
     c->prompt = dalloc<int>(R * d.n_text_ctx, o);
     c->done = dalloc<int>(1, o);
@@ -691,11 +697,19 @@ void encoder_layer(osw_ctx* c, int i, int nb) {
                            EPI_F32_RESID), CL_ENC_GEMM);
 }
 
-void encode(osw_ctx* c, const osw_window* wins, int n) {
+// slots (row refill): window i's cross K/V goes to decoder row slots[i] of a c->B-row layout
+void encode(osw_ctx* c, const osw_window* wins, int n, const int* slots = nullptr) {
     REQUIRE(c->finalized, "weights not finalized");
     REQUIRE(n >= 1 && n <= c->B, "window count out of range");
     const osw_dims& d = c->d;
     const int De = d.n_audio_state;
+    if (slots) {
+        std::vector<char> seen(c->B, 0);
+        for (int i = 0; i < n; ++i) {
+            REQUIRE(slots[i] >= 0 && slots[i] < c->B && !seen[slots[i]], "refill slots must be distinct rows < max_batch");
+            seen[slots[i]] = 1;
+        }
+    }
     std::vector<int> hw(3 * n);
     for (int i = 0; i < n; ++i) {
         REQUIRE(wins[i].clip >= 0 && wins[i].clip < c->n_clips, "window clip out of range");
@@ -755,6 +769,11 @@ void encode(osw_ctx* c, const osw_window* wins, int n) {
         GemmArgs g = gemm_plain(c->E, De, WH(c, "dec.crosskv.w"), WF(c, "dec.crosskv.b"), n * T_ENC,
                                 d.n_text_layer * 2 * d.n_text_state, De, c->XKV, 0, EPI_HEADS);
         g.heads_T = T_ENC; g.heads_H = d.n_text_head; g.heads_nb = n;
+        if (slots) {
+            HIPCHK(hipMemcpyAsync(c->slot_d, slots, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+            g.heads_nb = c->B;
+            g.heads_slot = c->slot_d;
+        }
         run_gemm(c, g, 0);
     }
     HIPCHK(hipGetLastError());
@@ -799,7 +818,7 @@ void decoder_step_fused(osw_ctx* c, int nb, int group, bool gather, const SelFus
         ProArgs pa{};
         pa.ln = ResLnArgs{embed ? nullptr : ps[last], ks, (int64_t)nb * D, bias, xs[xi], xs[xi ^ 1],
                           WF(c, ln + ".g"), WF(c, ln + ".b"), WH(c, "dec.tok"), WF(c, "dec.pos"), c->cur_tok, c->pos,
-                          ctx, D, d.n_vocab};
+                          ctx, D, d.n_vocab, c->row_pos ? 1 : 0};
         xi ^= 1;
         return pa;
     };
@@ -816,7 +835,7 @@ void decoder_step_fused(osw_ctx* c, int nb, int group, bool gather, const SelFus
         fused(PRO_RESLN, l == 0 ? resln(nullptr, p + ".ln1", true) : resln(WF(c, pp + ".fc2.b"), p + ".ln1", false),
               p + ".qkv.w", 3 * D, D);
         launch_dec_self_attn(ps[last], ks, WF(c, p + ".qkv.b"), c->kc + l * kv_layer, c->vc + l * kv_layer, c->pos,
-                             nb, H, ctx, c->dattn, lo_d, gather ? c->anc : nullptr, group, c->sel, c->stream);
+                             nb, H, ctx, c->dattn, lo_d, gather ? c->anc : nullptr, group, c->sel, c->stream, c->row_pos);
         plain(c->dattn, p + ".o.w", D, D);
         fused(PRO_RESLN, resln(WF(c, p + ".o.b"), p + ".ln2", false), p + ".xq.w", D, D);
         {
@@ -886,18 +905,18 @@ bool decoder_step(osw_ctx* c, int nb, int group, bool gather, const SelFuse* sf 
         return sf != nullptr && nb == 1;
     }
     // greedy batches of EX_MIN_ROWS.. windows: the E-form cross-attention (exattn.hip)
-    const bool eform = c->eform && group == 1 && !gather && nb >= EX_MIN_ROWS && nb <= 128 &&
+    const bool eform = c->eform && !c->row_pos && group == 1 && !gather && nb >= EX_MIN_ROWS && nb <= 128 &&
                        nb == c->n_encoded;
     static const bool no_gelu_pro = getenv("OSW_NO_GELU_PRO") != nullptr;  // A/B switch
     const bool gelu_pro = nb <= GELU_ROWS && !no_gelu_pro && 4 * D / skinny_ksplit(D, 4 * D) <= GELU_KC;
     // x = tok_emb[tok] + pos_emb[pos]; xdn = LN1_0(x)
     launch_dec_resid_ln(nullptr, 0, nb, D, nullptr, c->xd, WF(c, "dec.l0.ln1.g"), WF(c, "dec.l0.ln1.b"), c->xdn, lo_d,
-                        WH(c, "dec.tok"), WF(c, "dec.pos"), c->cur_tok, c->pos, ctx, d.n_vocab, c->stream);
+                        WH(c, "dec.tok"), WF(c, "dec.pos"), c->cur_tok, c->pos, ctx, d.n_vocab, c->stream, c->row_pos);
     for (int l = 0; l < L; ++l) {
         const std::string p = "dec.l" + std::to_string(l);
         int ks = partial(c->xdn, D, p + ".qkv.w", 3 * D, D);
         launch_dec_self_attn(c->part, ks, WF(c, p + ".qkv.b"), c->kc + l * kv_layer, c->vc + l * kv_layer, c->pos, nb,
-                             H, ctx, c->dattn, lo_d, gather ? c->anc : nullptr, group, c->sel, c->stream);
+                             H, ctx, c->dattn, lo_d, gather ? c->anc : nullptr, group, c->sel, c->stream, c->row_pos);
         ks = partial(c->dattn, D, p + ".o.w", D, D);
         launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".o.b"), c->xd, WF(c, p + ".ln2.g"), WF(c, p + ".ln2.b"),
                             c->xdn, lo_d, nullptr, nullptr, nullptr, nullptr, ctx, d.n_vocab, c->stream);
@@ -957,6 +976,59 @@ bool decoder_step(osw_ctx* c, int nb, int group, bool gather, const SelFuse* sf 
     gl.A_lo = c->xdn + lo_d;
     run_gemm(c, gl, 0);
     return false;
+}
+
+// The decode graph for `key` (CH steps of one_step), captured and instantiated on first use;
+// at most 16 per context, the least recently used one destroyed to make room.
+hipGraphExec_t decode_graph(osw_ctx* c, const std::vector<int64_t>& key, const std::function<void()>& one_step,
+                            int CH) {
+    auto hit = c->dgraphs.find(key);
+    if (hit != c->dgraphs.end()) {
+        hit->second.second = ++c->dgraph_tick;
+        return hit->second.first;
+    }
+    {
+        constexpr size_t kMaxGraphs = 16;
+        if (c->dgraphs.size() >= kMaxGraphs) {  // evict the least recently used
+            auto lru = c->dgraphs.begin();
+            for (auto it = c->dgraphs.begin(); it != c->dgraphs.end(); ++it)
+                if (it->second.second < lru->second.second) lru = it;
+            HIPCHK(hipStreamSynchronize(c->stream));
+            trace_graph(c, "destroy (LRU)");
+            HIPCHK(hipGraphExecDestroy(lru->second.first));
+            c->dgraphs.erase(lru);
+        }
+        HIPCHK(hipStreamSynchronize(c->stream));
+        hipGraph_t gr = nullptr;
+        hipGraphExec_t ge = nullptr;
+        // A sibling lane's encoder waits on the baton event, which this lane may have
+        // recorded on this stream: HIP refuses that wait while this stream captures
+        // ("dependency created on uncaptured work in another stream"), so no sibling
+        // enqueues an encoder (which holds the baton's mutex) during a capture.
+        std::unique_lock<std::mutex> no_encoder;
+        if (c->baton) no_encoder = std::unique_lock<std::mutex>(c->baton->mu);
+        c->capturing = true;
+        try {
+            trace_graph(c, "capture begin");
+            HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+            for (int i = 0; i < CH; ++i) one_step();
+            HIPCHK(hipStreamEndCapture(c->stream, &gr));
+            trace_graph(c, "capture end");
+        } catch (...) {
+            c->capturing = false;
+            hipGraph_t junk = nullptr;
+            (void)hipStreamEndCapture(c->stream, &junk);
+            if (junk) (void)hipGraphDestroy(junk);
+            throw;
+        }
+        c->capturing = false;
+        hipError_t e = hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0);
+        trace_graph(c, "instantiated");
+        (void)hipGraphDestroy(gr);
+        HIPCHK(e);
+        c->dgraphs[key] = {ge, ++c->dgraph_tick};
+        return ge;
+    }
 }
 
 void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) {
@@ -1059,51 +1131,7 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
                                     o->timestamp_begin, o->blank, o->first_lang, o->n_langs, o->suppress_blank,
                                     o->without_timestamps, o->max_initial_timestamp_index, beam, SP.num_hyp,
                                     SP.max_cand, lp_bits, group, it_bits, SP.budget ? 1 : 0};
-        auto hit = c->dgraphs.find(key);
-        if (hit != c->dgraphs.end()) {
-            c->dgraph = hit->second.first;
-            hit->second.second = ++c->dgraph_tick;
-        } else {
-            constexpr size_t kMaxGraphs = 16;
-            if (c->dgraphs.size() >= kMaxGraphs) {  // evict the least recently used
-                auto lru = c->dgraphs.begin();
-                for (auto it = c->dgraphs.begin(); it != c->dgraphs.end(); ++it)
-                    if (it->second.second < lru->second.second) lru = it;
-                HIPCHK(hipStreamSynchronize(c->stream));
-                trace_graph(c, "destroy (LRU)");
-                HIPCHK(hipGraphExecDestroy(lru->second.first));
-                c->dgraphs.erase(lru);
-            }
-            c->dgraph = nullptr;
-            HIPCHK(hipStreamSynchronize(c->stream));
-            hipGraph_t gr = nullptr;
-            // A sibling lane's encoder waits on the baton event, which this lane may have
-            // recorded on this stream: HIP refuses that wait while this stream captures
-            // ("dependency created on uncaptured work in another stream"), so no sibling
-            // enqueues an encoder (which holds the baton's mutex) during a capture.
-            std::unique_lock<std::mutex> no_encoder;
-            if (c->baton) no_encoder = std::unique_lock<std::mutex>(c->baton->mu);
-            c->capturing = true;
-            try {
-                trace_graph(c, "capture begin");
-                HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-                for (int i = 0; i < CH; ++i) one_step();
-                HIPCHK(hipStreamEndCapture(c->stream, &gr));
-                trace_graph(c, "capture end");
-            } catch (...) {
-                c->capturing = false;
-                hipGraph_t junk = nullptr;
-                (void)hipStreamEndCapture(c->stream, &junk);
-                if (junk) (void)hipGraphDestroy(junk);
-                throw;
-            }
-            c->capturing = false;
-            hipError_t e = hipGraphInstantiate(&c->dgraph, gr, nullptr, nullptr, 0);
-            trace_graph(c, "instantiated");
-            (void)hipGraphDestroy(gr);
-            HIPCHK(e);
-            c->dgraphs[key] = {c->dgraph, ++c->dgraph_tick};
-        }
+        c->dgraph = decode_graph(c, key, one_step, CH);
     }
     int steps = 0;
     {
@@ -1174,6 +1202,146 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
         r->no_speech_prob[b] = sp.nsp;
         r->language[b] = sp.lang;
     }
+}
+
+// Greedy decoding with row refill (osw_transcribe_refill): the decoder keeps c->B rows and
+// every row has its own step counter (pos[row], SelParams::pos_row), so when a window
+// finishes, a queued clip's window is encoded straight into that row's cross-K/V slot and
+// starts at position 0 beside rows that are mid-way.  A batch then costs what its windows'
+// own lengths cost instead of its longest window's.  Every row's arithmetic is the plain
+// greedy decode's (rows are independent in every kernel), so each clip's result equals
+// osw_transcribe_batch's for it.  Windows are admitted once refill_min rows are free (or
+// when no row is active); empty rows stay finished and are skipped by the attention kernels.
+void decode_refill(osw_ctx* c, int n_clips, const osw_decode_opts* o, osw_window_result* r, int refill_min) {
+    REQUIRE(o && r && r->tokens && r->n_tokens && r->sum_logprob && r->no_speech_prob && r->language,
+            "null decode argument");
+    REQUIRE(!(o->temperature > 0.f) && o->beam_size <= 1, "row refill decodes greedily (temperature 0, beam_size 1)");
+    REQUIRE(o->n_prefix == 0, "row refill takes no prefix tokens");
+    REQUIRE(!r->logits_dump, "row refill has no logits dump");
+    const osw_dims& d = c->d;
+    const int V = d.n_vocab;
+    REQUIRE(V <= SEL_SPLIT * 4096, "vocabulary too large for the selection kernels");
+    const int R = c->B;
+    REQUIRE(R <= c->R, "decoder rows");
+    const int P = 3 + (o->without_timestamps ? 1 : 0);
+    const int max_len = std::min(o->max_length > 0 ? o->max_length : d.n_text_ctx, d.n_text_ctx);
+    REQUIRE(P < max_len, "prompt longer than max_length");
+    const int max_tok = std::max(1, max_len - P);
+    refill_min = std::max(1, std::min(refill_min, R));
+    std::vector<unsigned> mask((V + 31) / 32, 0u);
+    for (int i = 0; i < o->n_suppress; ++i) {
+        const int t = o->suppress_tokens[i];
+        if (t >= 0 && t < V) mask[t >> 5] |= 1u << (t & 31);
+    }
+    SelParams SP{};
+    SP.prompt_len = P; SP.sot_pos = 0; SP.lang_pos = 1; SP.max_length = max_len;
+    SP.V = V; SP.eot = o->eot; SP.no_speech = o->no_speech; SP.no_ts = o->no_timestamps; SP.tb = o->timestamp_begin;
+    SP.blank = o->blank; SP.first_lang = o->first_lang; SP.n_langs = o->n_langs;
+    SP.suppress_blank = o->suppress_blank; SP.with_ts = o->without_timestamps ? 0 : 1;
+    SP.max_init_ts = o->max_initial_timestamp_index;
+    SP.beam = 1; SP.num_hyp = 1; SP.max_cand = 1;
+    SP.length_penalty = o->length_penalty;
+    SP.inv_temp = 0.f;
+    HIPCHK(hipMemcpyAsync(c->seed_d, &o->seed, 8, hipMemcpyHostToDevice, c->stream));
+    SP.seed = c->seed_d;
+    SP.budget = o->token_budget ? c->budget : nullptr;
+    SP.pos_row = 1;
+    HIPCHK(hipMemcpyAsync(c->supmask, mask.data(), mask.size() * 4, hipMemcpyHostToDevice, c->stream));
+    // every row starts finished (nothing to step until a window is admitted)
+    std::vector<SelState> st(R);
+    for (auto& q : st) q = SelState{}, q.done = 1;
+    HIPCHK(hipMemcpyAsync(c->sel, st.data(), (size_t)R * sizeof(SelState), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemsetAsync(c->pos, 0, (size_t)R * 4, c->stream));
+    HIPCHK(hipMemsetAsync(c->cur_tok, 0, (size_t)R * 4, c->stream));
+    HIPCHK(hipMemsetAsync(c->prompt, 0, (size_t)R * P * 4, c->stream));
+    struct RowPos {
+        osw_ctx* c;
+        ~RowPos() { c->row_pos = false; c->n_encoded = 0; }
+    } row_pos_scope{c};
+    c->row_pos = true;
+    auto one_step = [&] {
+        decoder_step(c, R, 1, false, nullptr);
+        launch_select(c->logits, R, c->pos, SP, c->prompt, c->supmask, c->sel, c->cur_tok, c->tokens, max_tok,
+                      c->selp, c->sel_arrive, true, c->bcand, c->stream);
+    };
+    const int CH = 8;
+    const bool graph = c->use_graph && !c->prof_eager;
+    hipGraphExec_t ge = nullptr;
+    if (graph) {
+        int32_t lp_bits;
+        std::memcpy(&lp_bits, &SP.length_penalty, 4);
+        // (the -1 tail keeps refill keys apart from decode()'s)
+        const std::vector<int64_t> key = {R, P, 0, max_len, o->eot, o->no_speech, o->no_timestamps,
+                                          o->timestamp_begin, o->blank, o->first_lang, o->n_langs, o->suppress_blank,
+                                          o->without_timestamps, o->max_initial_timestamp_index, 1, 1,
+                                          1, lp_bits, 1, 0, SP.budget ? 1 : 0, -1};
+        ge = decode_graph(c, key, one_step, CH);
+    }
+    std::vector<int> row_clip(R, -1), pack, toks((size_t)R * max_tok);
+    int next = 0, active = 0, steps = 0;
+    while (true) {
+        std::vector<int> free_rows;
+        for (int i = 0; i < R; ++i)
+            if (row_clip[i] < 0) free_rows.push_back(i);
+        const int left = n_clips - next;
+        if (left > 0 && (active == 0 || (int)free_rows.size() >= std::min(refill_min, left))) {
+            const int k = std::min((int)free_rows.size(), left);
+            std::vector<osw_window> wins(k);
+            std::vector<int> slots(k);
+            pack.assign((size_t)k * (2 + P), 0);
+            for (int i = 0; i < k; ++i) {
+                const int clip = next + i, row = free_rows[i];
+                wins[i] = osw_window{clip, 0, std::max(1, std::min(N_FR, c->nframes[clip] - 1))};
+                slots[i] = row;
+                int* e = &pack[(size_t)i * (2 + P)];
+                e[0] = row;
+                e[1] = o->token_budget ? o->token_budget[clip] : 0;
+                e[2] = o->sot;
+                e[3] = o->language_tokens ? o->language_tokens[clip] : o->language_token;  // -1: detect
+                e[4] = o->task_token;
+                if (o->without_timestamps) e[5] = o->no_timestamps;
+                row_clip[row] = clip;
+            }
+            encode(c, wins.data(), k, slots.data());
+            c->n_encoded = 0;
+            HIPCHK(hipMemcpyAsync(c->refill_pack, pack.data(), pack.size() * 4, hipMemcpyHostToDevice, c->stream));
+            launch_refill_rows(c->refill_pack, k, P, c->prompt, SP.budget ? c->budget : nullptr, c->cur_tok, c->pos,
+                               c->sel, c->stream);
+            HIPCHK(hipGetLastError());
+            next += k;
+            active += k;
+        }
+        if (active == 0) break;
+        if (graph) {
+            trace_graph(c, "launch");
+            HIPCHK(hipGraphLaunch(ge, c->stream));
+        } else {
+            for (int i = 0; i < CH; ++i) one_step();
+        }
+        HIPCHK(hipGetLastError());
+        steps += CH;
+        HIPCHK(hipMemcpyAsync(st.data(), c->sel, (size_t)R * sizeof(SelState), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        bool fin = false;
+        for (int i = 0; i < R; ++i) fin |= row_clip[i] >= 0 && st[i].done;
+        if (!fin) continue;
+        HIPCHK(hipMemcpyAsync(toks.data(), c->tokens, toks.size() * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        for (int i = 0; i < R; ++i) {
+            const int clip = row_clip[i];
+            if (clip < 0 || !st[i].done) continue;
+            const SelState& q = st[i];
+            const int n = std::min(q.n_sampled, std::min(max_tok, r->max_tokens));
+            r->n_tokens[clip] = n;
+            for (int j = 0; j < n; ++j) r->tokens[(size_t)clip * r->max_tokens + j] = toks[(size_t)i * max_tok + j];
+            r->sum_logprob[clip] = q.sum_lp;
+            r->no_speech_prob[clip] = q.nsp;
+            r->language[clip] = q.lang;
+            row_clip[i] = -1;
+            --active;
+        }
+    }
+    c->pf.decode_steps = steps;
 }
 
 // ------------------------------ mel ----------------------------------------
@@ -1628,6 +1796,21 @@ int osw_transcribe_batch(osw_ctx* c, const int16_t* pcm, const int64_t* offsets,
             wins[i] = osw_window{i, 0, std::max(1, std::min(N_FR, c->nframes[i] - 1))};
         encode(c, wins.data(), n_clips);
         decode(c, n_clips, opts, res);
+        resolve_events(c);
+    });
+}
+
+int osw_transcribe_refill(osw_ctx* c, const int16_t* pcm, const int64_t* offsets, int32_t n_clips,
+                          int32_t pcm_on_device, const osw_decode_opts* opts, osw_window_result* res,
+                          int32_t refill_min) {
+    return guard([&] {
+        REQUIRE(c, "null ctx");
+        std::lock_guard<std::mutex> lk(c->mu);
+        DeviceScope dev_scope_((c->device));
+        REQUIRE(n_clips >= 1, "n_clips out of range");
+        LaneCall call_(c);
+        log_mel(c, pcm, offsets, n_clips, pcm_on_device, nullptr);
+        decode_refill(c, n_clips, opts, res, refill_min);
         resolve_events(c);
     });
 }

@@ -26,13 +26,14 @@ struct ResLnArgs {
     float* x_out;       // updated residual stream (may alias x_in in the standalone kernel)
     const float* g;
     const float* b;
-    const h16* tok_emb;  // embedding entry: x' = tok_emb[tok[r]] + pos_emb[min(*pos, ctx-1)]
+    const h16* tok_emb;  // embedding entry: x' = tok_emb[tok[r]] + pos_emb[min(pos, ctx-1)]
     const float* pos_emb;
     const int* tok;
     const int* pos;
     int ctx;
     int D;
     int V;              // rows of tok_emb: an id outside [0, V) is clamped into it
+    int pos_row;        // 1: row r's position is pos[r] (row refill), 0: every row's is pos[0]
 };
 
 // rows r0 .. r0+nr-1 (nr <= NR); emit(r, c, y) receives every LayerNorm output;
@@ -46,8 +47,6 @@ __device__ __forceinline__ void resln_rows(const ResLnArgs& A, int r0, int nr, b
     const bool h4 = 4 * t < D, h1 = 1024 + t < D;
     const int c4 = h4 ? 4 * t : 0, c1 = h1 ? 1024 + t : 0;  // clamped: every load stays in the row
     float v[NR][5];
-    int pos = 0;
-    if (!A.part) pos = min(*A.pos, A.ctx - 1);
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
 #pragma unroll
@@ -86,6 +85,7 @@ __device__ __forceinline__ void resln_rows(const ResLnArgs& A, int r0, int nr, b
         } else {
             const int tk = min(max(A.tok[r0 + r], 0), A.V - 1);  // defence in depth: select never emits one
             const h16x4 e4 = *(const h16x4*)(A.tok_emb + (int64_t)tk * D + c4);
+            const int pos = min(A.pos[A.pos_row ? r0 + r : 0], A.ctx - 1);
             const float* pe = A.pos_emb + (int64_t)pos * D;
             a4 = f32x4{(float)e4[0], (float)e4[1], (float)e4[2], (float)e4[3]} + *(const f32x4*)(pe + c4);
             a1 = (float)A.tok_emb[(int64_t)tk * D + c1] + pe[c1];

@@ -16,6 +16,7 @@ rank, so the RCCL call sequence is identical across ranks.
 """
 from __future__ import annotations
 
+import dataclasses
 from collections import deque
 from concurrent.futures import ThreadPoolExecutor
 
@@ -107,6 +108,50 @@ class DataParallelTranscriber:
         while inflight:
             outs = inflight.popleft().result()
             res.append((outs, self.gather(outs)))
+        return res
+
+    def run_steps_refill(self, all_pcm, k: int, refill_min: int = 8):
+        """k steps' clips with row refill (WhisperEngine.transcribe_refill): step i goes to
+        lane i % lanes as in run_steps, but each lane takes ALL of its steps' clips in one
+        call, so its decoder rows stay full across the step boundaries (a finished window's
+        row takes the next clip) instead of every batch waiting for its longest window.
+        Greedy only.  Collectives (scatter, gather) run in step order on the calling
+        thread, as in run_steps.  Returns [(local outputs, gathered ids or None)] per step."""
+        torch = self.torch
+        nl = len(self.lanes)
+        steps = [[i for i in range(k) if i % nl == lane] for lane in range(nl)]
+        bufs = [torch.empty((len(st) * self.B, self.S), dtype=torch.int16, device=self.device) if st else None
+                for st in steps]
+        for i in range(k):  # the scatters in step order (identical on every rank)
+            lane, j = i % nl, i // nl
+            self.scatter(all_pcm, 0)
+            bufs[lane][j * self.B:(j + 1) * self.B].copy_(self.shards[0])
+        self._sync()
+        cfg = self.cfg
+
+        def lane_call(lane):
+            n = len(steps[lane]) * self.B
+            c = cfg
+            if cfg.token_budget is not None:
+                c = dataclasses.replace(cfg, token_budget=tuple(cfg.token_budget) * len(steps[lane]))
+            eng = self.lanes[lane]
+            if self.device.type == "cuda":
+                offs = np.arange(n + 1, dtype=np.int64) * self.S
+                return eng.transcribe_refill(None, c, device_pcm=bufs[lane].data_ptr(), offsets=offs,
+                                             refill_min=refill_min)
+            return eng.transcribe_refill(list(bufs[lane].numpy()), c, refill_min=refill_min)
+
+        lanes = [lane for lane in range(nl) if steps[lane]]
+        if self.pool is None:
+            outs = {lane: lane_call(lane) for lane in lanes}
+        else:
+            futs = {lane: self.pool.submit(lane_call, lane) for lane in lanes}
+            outs = {lane: f.result() for lane, f in futs.items()}
+        res = []
+        for i in range(k):
+            lane, j = i % nl, i // nl
+            o = outs[lane][j * self.B:(j + 1) * self.B]
+            res.append((o, self.gather(o)))
         return res
 
     def close(self) -> None:

@@ -67,7 +67,7 @@ def parse(argv=None):
                     help="BASELINE configs[4]: concurrent /v1/audio/stream sessions simulated through the backend "
                          "(0 = skip)")
     ap.add_argument("--stream-speech-s", type=float, default=6.0, help="seconds of speech per streaming session")
-    ap.add_argument("--refill-min", type=int, default=8,
+    ap.add_argument("--refill-min", type=int, default=24,
                     help="row refill (realistic lengths): admit queued clips once this many rows are free")
     ap.add_argument("--realistic-steps", type=int, default=9,
                     help="also time this many steps with realistic output lengths (random weights never emit "

@@ -410,10 +410,16 @@ void build_weight_table(osw_ctx* c) {
     };
     frag("dec.tok", d.n_vocab, Dd);
     frag("dec.crosskv.w", L * 2 * Dd, De);  // the E-form V projection streams its V rows
-    // E-form cross-attention (exattn.hip): every layer's Wk as [H][D][64], derived from
-    // dec.crosskv.w like the fragment-major copies (+ 13 MB at turbo)
-    add_tensor(c, "dec.crosskv.kT", L * Dd * De, true);
-    c->w["dec.crosskv.kT"].set = true;
+    // E-form cross-attention (exattn.hip, OSW_EFORM=1): every layer's Wk as [H][D][64],
+    // derived from dec.crosskv.w like the fragment-major copies (+ 13 MB at turbo); only in
+    // contexts created with the E-form on (siblings share the parent's table)
+    {
+        const char* ef = getenv("OSW_EFORM");
+        if ((ef ? atoi(ef) != 0 : kEformDefault) && Dd == De) {
+            add_tensor(c, "dec.crosskv.kT", L * Dd * De, true);
+            c->w["dec.crosskv.kT"].set = true;
+        }
+    }
     for (int i = 0; i < d.n_text_layer; ++i) {
         const std::string p = "dec.l" + std::to_string(i);
         frag(p + ".qkv.w", 3 * Dd, Dd);
@@ -464,7 +470,7 @@ const h16* WFR(osw_ctx* c, const std::string& n) {
 // rewrite the fragment-major copy after the matrix was written (on the context's stream)
 void pack_frag(osw_ctx* c, const std::string& n) {
     const Tensor& t = W(c, n);
-    if (n == "dec.crosskv.w" && c->d.n_text_state == c->d.n_audio_state) {
+    if (n == "dec.crosskv.w" && c->w.count("dec.crosskv.kT")) {
         launch_ex_pack_kT((const h16*)t.ptr, c->d.n_text_layer, c->d.n_text_state, (h16*)W(c, "dec.crosskv.kT").ptr,
                           c->stream);
         HIPCHK(hipGetLastError());
@@ -605,7 +611,7 @@ void setup_workspace(osw_ctx* c) {
         // OSW_EFORM=0/1 overrides the default (read per context, so tests can hold both forms)
         const char* ef = getenv("OSW_EFORM");
         const bool off = ef ? atoi(ef) == 0 : !kEformDefault;
-        c->eform = !off && De == Dd && exattn_supported(D, H);
+        c->eform = !off && De == Dd && exattn_supported(D, H) && c->w.count("dec.crosskv.kT");
         if (c->eform) {
             const int64_t HP = EX_HP, BE = std::min<int64_t>(B, 128);
             c->exq_lo = BE * HP * D;

@@ -29,6 +29,7 @@
 //   Oᵀ += E_tileᵀ · Pᵀ  v_mfma_f32_16x16x16_f16: A = E columns (ds_read_b64_tr_b16), B = P
 //                       (hi, lo) straight from the softmax registers
 #include "decode.h"
+#include "ldsasm.h"
 
 #include <cstdlib>
 
@@ -46,45 +47,6 @@ __device__ __forceinline__ int ex_qfrag(int h, int j) {
     return (((j >> 5) * 2 + (h >> 4)) * 64 + 16 * ((j & 31) >> 3) + (h & 15)) * 8 + (j & 7);
 }
 
-// E-tile LDS reads as inline asm: hipcc would otherwise drain vmcnt(0) before every LDS read
-// (it cannot tell the ring slot being read from the slots the LDS-DMA is still filling),
-// which would stall each tile for the two tiles in flight.  The caller waits lgkmcnt.
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ unsigned lds_addr(const h16* p) { return (unsigned)(uintptr_t)(OSW_LDS const h16*)p; }
-__device__ __forceinline__ h16x8 ex_read_row(const h16* p) {
-    u32x4 v;
-    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(lds_addr(p)) : "memory");
-    return __builtin_bit_cast(h16x8, v);
-}
-__device__ __forceinline__ h16x4 ex_read_tr(const h16* p) {
-    u32x2 v;
-    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(lds_addr(p)) : "memory");
-    return __builtin_bit_cast(h16x4, v);
-}
-__device__ __forceinline__ float ex_read_f32(const float* p) {
-    float v;
-    asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"((unsigned)(uintptr_t)(OSW_LDS const float*)p) : "memory");
-    return v;
-}
-__device__ __forceinline__ void ex_wait_lgkm() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-// after ex_wait_lgkm(): the values are defined by an (empty) asm ordered after the wait, so
-// nothing the compiler schedules can consume them earlier
-template <class T>
-__device__ __forceinline__ void ex_landed(T& v) { asm volatile("" : "+v"(v)); }
-
-template <int N>
-__device__ __forceinline__ void ex_wait_vmcnt() {
-    static_assert(N >= 0 && N < 64, "vmcnt range");
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// LDS writes of every wave visible, the wave's outstanding global loads untouched
-__device__ __forceinline__ void ex_lds_barrier() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-}
 
 // q' = (Wk_h^T q16_h) / 8 for every row and head; grid (H, D / 128), 256 threads.
 // q16 = fp16(bias + Σ_k part[k]) (slabs summed in order; the rounding point the oracle's
@@ -239,8 +201,8 @@ __global__ __launch_bounds__(NW * 64, 1) void exattn_kernel(const h16* __restric
     for (int s = 0; s < NS; ++s)
 #pragma unroll
         for (int ht = 0; ht < 2; ++ht) {
-            ex_landed(qh[s][ht]);
-            ex_landed(ql[s][ht]);
+            asm_landed(qh[s][ht]);
+            asm_landed(ql[s][ht]);
         }
 
     // a landed tile into registers: E rows (the scores' A operand) and E columns by
@@ -252,22 +214,22 @@ __global__ __launch_bounds__(NW * 64, 1) void exattn_kernel(const h16* __restric
     auto read_tile = [&](int t, h16x8 (&arow)[NS], h16x8 (&acol)[NM]) {
         const h16* El = Es[wv][t % EX_NBUF];
 #pragma unroll
-        for (int s = 0; s < NS; ++s) arow[s] = ex_read_row(&El[li * JW + 8 * ((4 * s + g) ^ ex_swz(li))]);
+        for (int s = 0; s < NS; ++s) arow[s] = asm_read_b128(&El[li * JW + 8 * ((4 * s + g) ^ ex_swz(li))]);
         h16x4 tr[NM][2];
 #pragma unroll
         for (int m = 0; m < NM; ++m)
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 const int row = 8 * (g >> 1) + 4 * r + trq, lc = 4 * m + 2 * (g & 1) + (trp >> 1);
-                tr[m][r] = ex_read_tr(&El[row * JW + 8 * (lc ^ ex_swz(row)) + 4 * (trp & 1)]);
+                tr[m][r] = asm_read_tr(&El[row * JW + 8 * (lc ^ ex_swz(row)) + 4 * (trp & 1)]);
             }
-        ex_wait_lgkm();
+        asm_wait_lgkm();
 #pragma unroll
-        for (int s = 0; s < NS; ++s) ex_landed(arow[s]);
+        for (int s = 0; s < NS; ++s) asm_landed(arow[s]);
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
-            ex_landed(tr[m][0]);
-            ex_landed(tr[m][1]);
+            asm_landed(tr[m][0]);
+            asm_landed(tr[m][1]);
             acol[m] = __builtin_shufflevector(tr[m][0], tr[m][1], 0, 1, 2, 3, 4, 5, 6, 7);
         }
         if (t + EX_NBUF < ntiles) stage(t % EX_NBUF, t + EX_NBUF);
@@ -300,10 +262,10 @@ __global__ __launch_bounds__(NW * 64, 1) void exattn_kernel(const h16* __restric
             const float* sp = (const float*)&Sp[0][head >> 4][16 * (key >> 2) + (head & 15)] + (key & 3);
             float part[NW];
 #pragma unroll
-            for (int u = 0; u < NW; ++u) part[u] = ex_read_f32(sp + u * 2 * 64 * 4);
-            ex_wait_lgkm();
+            for (int u = 0; u < NW; ++u) part[u] = asm_read_f32(sp + u * 2 * 64 * 4);
+            asm_wait_lgkm();
 #pragma unroll
-            for (int u = 0; u < NW; ++u) ex_landed(part[u]);
+            for (int u = 0; u < NW; ++u) asm_landed(part[u]);
             float s = part[0];
 #pragma unroll
             for (int u = 1; u < NW; ++u) s += part[u];
@@ -336,24 +298,24 @@ __global__ __launch_bounds__(NW * 64, 1) void exattn_kernel(const h16* __restric
     // and k+2 in flight
     auto wait_tile = [&](int k) {
         const int after = min(ntiles - 1 - k, 2);
-        after == 2 ? ex_wait_vmcnt<2 * NI>() : after == 1 ? ex_wait_vmcnt<NI>() : ex_wait_vmcnt<0>();
+        after == 2 ? asm_wait_vmcnt<2 * NI>() : after == 1 ? asm_wait_vmcnt<NI>() : asm_wait_vmcnt<0>();
     };
     h16x8 arow[NS], acol[NM];
     wait_tile(0);
     read_tile(0, arow, acol);
     scores(arow);
-    ex_lds_barrier();
+    asm_lds_barrier();
     softmax(0);
-    ex_lds_barrier();
+    asm_lds_barrier();
     for (int t = 0; t < ntiles; ++t) {
-        // (LDS reads as asm throughout the loop: see ex_read_row)
-        h16x8 bh = ex_read_row(&Pt[0][lane & 31][8 * (lane >> 5)]);
-        h16x8 bl = ex_read_row(&Pt[1][lane & 31][8 * (lane >> 5)]);
-        float alpha = ex_read_f32(&Al[lane & 31]);
-        ex_wait_lgkm();
-        ex_landed(bh);
-        ex_landed(bl);
-        ex_landed(alpha);
+        // (LDS reads as asm throughout the loop: ldsasm.h)
+        h16x8 bh = asm_read_b128(&Pt[0][lane & 31][8 * (lane >> 5)]);
+        h16x8 bl = asm_read_b128(&Pt[1][lane & 31][8 * (lane >> 5)]);
+        float alpha = asm_read_f32(&Al[lane & 31]);
+        asm_wait_lgkm();
+        asm_landed(bh);
+        asm_landed(bl);
+        asm_landed(alpha);
         if (__any(alpha != 1.0f)) {
 #pragma unroll
             for (int m = 0; m < NM; ++m) o[m] *= alpha;
@@ -367,9 +329,9 @@ __global__ __launch_bounds__(NW * 64, 1) void exattn_kernel(const h16* __restric
             wait_tile(t + 1);
             read_tile(t + 1, arow, acol);
             scores(arow);
-            ex_lds_barrier();
+            asm_lds_barrier();
             softmax(t + 1);
-            ex_lds_barrier();
+            asm_lds_barrier();
         }
     }
     // ---- partials: ws[w][c][head] = {m, l, pad x 6, O[D]} (plain stores: ex_merge is the next launch)

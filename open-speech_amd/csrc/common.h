@@ -39,8 +39,14 @@ __device__ __forceinline__ float erf_fast(float x) {
     return copysignf(y, x);
 }
 
+// The result is rounded to fp32 before any fp16 conversion: without the opaque move the
+// compiler fused the last multiply into the conversion (v_fma_mixlo_f16, one rounding) in
+// some epilogues and not in others (v_mul_f32 + v_cvt_pk_f16_f32), so the same GELU
+// input could leave two tile kernels as different fp16 values
 __device__ __forceinline__ float gelu_erf(float x) {
-    return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f));
+    float r = 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f));
+    asm("" : "+v"(r));
+    return r;
 }
 
 // Lane exchange v[lane ^ O] without the LDS pipe: DPP for O <= 8 (quad_perm, half-row

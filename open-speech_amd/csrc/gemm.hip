@@ -302,7 +302,11 @@ __device__ __forceinline__ int acc_col(int wn, int ni) { return IL ? (ni >> 1) *
 // Output rows leave through nontemporal stores: the encoder's activations (0.5-2 GB per
 // GEMM at 64 windows) stream past the MALL instead of evicting the weights and the
 // next GEMM's operand panels (8p GEMMs 4-7 % and the attention after them 6 % faster).
-template <int EPI, bool IL = false>
+// TR (8-phase kernel, IL): the accumulators are transposed (the kernel swaps the MFMA
+// operands), lane l of block (mi, ni) holding C[row + (l & 15)][col + 4 (l >> 4) + e], so the
+// image takes one 8-B (fp16) / 16-B (fp32) write per block instead of four 2-B / 4-B ones
+// (fc1 at 64 windows 1488 -> 1432 us, + GELU 1694 -> 1627 us; profiles/r04_s_epilogue.jsonl, r04_t_epilogue_forms.jsonl)
+template <int EPI, bool IL = false, bool TR = false>
 __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], int m0, int n0, int wm,
                                                 int wn, char* smem, int tid) {
     const int lane = tid & 63;
@@ -315,6 +319,21 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
         constexpr int NH = IL ? 2 : 1;
 #pragma unroll
         for (int half = 0; half < NH; ++half) {
+        if constexpr (TR) {
+#pragma unroll
+            for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni) {
+                    if (IL && (mi >> 2) != half) continue;
+                    const int row = acc_row<IL>(wm, mi) + (lane & 15);
+                    const int col = acc_col<IL>(wn, ni) + 4 * (lane >> 4);
+                    const int n = min(n0 + col, g.N - 4);
+                    h16x4 v;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = (h16)epi_value<EPI>(g, m0 + row, n + e, acc[mi][ni][e]);
+                    *(h16x4*)&T[ep16(row, col)] = v;
+                }
+        } else
 #pragma unroll
         for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
@@ -350,7 +369,21 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
     } else {
         float* T = (float*)smem;
         for (int half = 0; half < 2; ++half) {
-            if (IL || wm == half) {
+            if (TR && IL) {
+#pragma unroll
+                for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < 4; ++ni) {
+                        if ((mi >> 2) != half) continue;
+                        const int row = acc_row<IL>(wm, mi) - half * 128 + (lane & 15);
+                        const int col = acc_col<IL>(wn, ni) + 4 * (lane >> 4);
+                        const int n = min(n0 + col, g.N - 4);
+                        f32x4 v;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = epi_value<EPI>(g, m0 + half * 128 + row, n + e, acc[mi][ni][e]);
+                        *(f32x4*)&T[ep32(row, col)] = v;
+                    }
+            } else if (IL || wm == half) {
 #pragma unroll
                 for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
@@ -546,7 +579,7 @@ __device__ __forceinline__ void lds_sync() {  // LDS accesses of every wave done
 // in flight into ring buffer 0 (NEXT0): the image lives in buffer 1 (the upper 64 KiB) and
 // the tile leaves in passes that fit it — fp16: two 128-row halves, fp32: four 64-row
 // quarters — with LDS-only barriers, so the prefetch loads stay in flight throughout.
-template <int EPI>
+template <int EPI, bool TR = false>
 __device__ __forceinline__ void staged_epilogue_next0(const GemmArgs& g, f32x4 (&acc)[8][4], int m0, int n0, int wm,
                                                       int wn, char* smem, int tid) {
     const int lane = tid & 63;
@@ -558,6 +591,22 @@ __device__ __forceinline__ void staged_epilogue_next0(const GemmArgs& g, f32x4 (
     for (int pass = 0; pass < NP; ++pass) {
         if constexpr (F16) {
             h16* T = (h16*)(smem + 4 * HT * 2);
+            if constexpr (TR) {
+#pragma unroll
+                for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < 4; ++ni) {
+                        if ((mi >> 2) != pass) continue;
+                        const int row = acc_row<true>(wm, mi) - pass * PR + (lane & 15);
+                        const int col = acc_col<true>(wn, ni) + 4 * (lane >> 4);
+                        const int n = min(n0 + col, g.N - 4);
+                        h16x4 v;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            v[e] = (h16)epi_value<EPI>(g, m0 + pass * PR + row, n + e, acc[mi][ni][e]);
+                        *(h16x4*)&T[ep16(row, col)] = v;
+                    }
+            } else
 #pragma unroll
             for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
@@ -592,7 +641,21 @@ __device__ __forceinline__ void staged_epilogue_next0(const GemmArgs& g, f32x4 (
         } else {
             float* T = (float*)(smem + 4 * HT * 2);
             // pass p = rows [64 p, 64 p + 64): wave rows (mi >> 2) * 128 + wm * 64
-            if (wm == (pass & 1)) {
+            if (TR && wm == (pass & 1)) {
+#pragma unroll
+                for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < 4; ++ni) {
+                        if ((mi >> 2) != (pass >> 1)) continue;
+                        const int row = acc_row<true>(wm, mi) - pass * PR + (lane & 15);
+                        const int col = acc_col<true>(wn, ni) + 4 * (lane >> 4);
+                        const int n = min(n0 + col, g.N - 4);
+                        f32x4 v;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = epi_value<EPI>(g, m0 + pass * PR + row, n + e, acc[mi][ni][e]);
+                        *(f32x4*)&T[ep32(row, col)] = v;
+                    }
+            } else if (wm == (pass & 1)) {
 #pragma unroll
                 for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
@@ -631,7 +694,7 @@ __device__ __forceinline__ void staged_epilogue_next0(const GemmArgs& g, f32x4 (
 
 // NEXT0: K-tile 0 of this tile was staged by the previous tile (pre0) / stage the next
 // tile's K-tile 0 (next_bid >= 0) before this tile's epilogue
-template <int EPI, bool NOEPI>
+template <int EPI, int DBG>
 __device__ __forceinline__ void gemm8p_tile(const GemmArgs& g, int bid, h16* smem, int tid, bool pre0 = false,
                                             int next_bid = -1) {
     const int wave = tid >> 6, lane = tid & 63;
@@ -691,8 +754,13 @@ __device__ __forceinline__ void gemm8p_tile(const GemmArgs& g, int bid, h16* sme
 #pragma unroll
             for (int nt = 0; nt < 2; ++nt) {
                 f32x4 c = acc[a * 4 + mt][b * 2 + nt];
-                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mt][0], bf[nt][0], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mt][1], bf[nt][1], c, 0, 0, 0);
+                if constexpr (DBG != 2) {  // transposed: Cᵀ = W Aᵀ, the same products in the same K order
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[nt][0], af[mt][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[nt][1], af[mt][1], c, 0, 0, 0);
+                } else {
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mt][0], bf[nt][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mt][1], bf[nt][1], c, 0, 0, 0);
+                }
                 acc[a * 4 + mt][b * 2 + nt] = c;
             }
         __builtin_amdgcn_s_setprio(0);
@@ -763,10 +831,10 @@ __device__ __forceinline__ void gemm8p_tile(const GemmArgs& g, int bid, h16* sme
             for (int i = 0; i < 2; ++i)
                 __builtin_amdgcn_global_load_lds((const void*)src8p(g, nm0, nn0, H, i, wave, lane),
                                                  (OSW_LDS void*)(smem + H * HT + (i * 8 + wave) * 8 * BK), 16, 0, 0);
-        if constexpr (!NOEPI) staged_epilogue_next0<EPI>(g, acc, m0, n0, wm, wn, (char*)smem, tid);
+        if constexpr (DBG != 1) staged_epilogue_next0<EPI, DBG != 2>(g, acc, m0, n0, wm, wn, (char*)smem, tid);
         return;
     }
-    if constexpr (NOEPI) {
+    if constexpr (DBG == 1) {
         float t = 0.f;
 #pragma unroll
         for (int i = 0; i < 8; ++i)
@@ -774,7 +842,7 @@ __device__ __forceinline__ void gemm8p_tile(const GemmArgs& g, int bid, h16* sme
             for (int j = 0; j < 4; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
         if (t == 1234.5f) ((float*)g.C)[tid] = t;  // keeps the loop live
     } else {
-        staged_epilogue<EPI, true>(g, acc, m0, n0, wm, wn, (char*)smem, tid);
+        staged_epilogue<EPI, true, DBG != 2>(g, acc, m0, n0, wm, wn, (char*)smem, tid);
     }
 }
 
@@ -786,7 +854,9 @@ __device__ __forceinline__ void gemm8p_tile(const GemmArgs& g, int bid, h16* sme
 // dispatches by 17-30 us each; every decoder kernel of a greedy step must
 // then fit beside an encoder workgroup (<= 30 KiB of LDS, <= 80 VGPRs); the 64-row logits
 // GEMM (80 KiB) does not.  4832 vs 4789 audio-s/s (12 steps, two runs each).
-template <int EPI, bool NOEPI = false>  // NOEPI: no epilogue (debug variant 9: main-loop time alone)
+// DBG (debug variants): 1 no epilogue (9: main-loop time alone), 2 the accumulators not
+// transposed (the round-3 epilogue; 12-14)
+template <int EPI, int DBG = 0>
 __global__ __launch_bounds__(GNT, 1) void gemm8p_kernel(GemmArgs g) {
     extern __shared__ __attribute__((aligned(16))) h16 smem[];  // [2][A0 A1 W0 W1][128*64]
     const int nwg = ((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
@@ -801,18 +871,18 @@ __global__ __launch_bounds__(GNT, 1) void gemm8p_kernel(GemmArgs g) {
         int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
         const int nxt = next0 && vb + (int)gridDim.x < nwg ? vb + (int)gridDim.x : -1;
-        gemm8p_tile<EPI, NOEPI>(g, vb, smem, tid, pre0, nxt);
+        gemm8p_tile<EPI, DBG>(g, vb, smem, tid, pre0, nxt);
         pre0 = nxt >= 0;
         if (!pre0) __syncthreads();  // the epilogue's LDS image is the next tile's operand ring
     }
 }
 
-template <int EPI, bool NOEPI = false>
+template <int EPI, int DBG = 0>
 void launch8p(const GemmArgs& g0, hipStream_t s) {
     static bool attr = false;
     constexpr int lds = EPI_LDS > 8 * HT * 2 ? EPI_LDS : 8 * HT * 2;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gemm8p_kernel<EPI, NOEPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)gemm8p_kernel<EPI, DBG>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   lds);
         attr = true;
     }
@@ -849,7 +919,7 @@ void launch8p(const GemmArgs& g0, hipStream_t s) {
         return std::max(8, cus * 3 / 4 / 8 * 8);
     }();
     const int grid_cap = per_tile ? 1 << 30 : g.share_cus ? shared_cap : cus;
-    gemm8p_kernel<EPI, NOEPI><<<std::min(nwg, std::max(8, grid_cap)), GNT, lds, s>>>(g);
+    gemm8p_kernel<EPI, DBG><<<std::min(nwg, std::max(8, grid_cap)), GNT, lds, s>>>(g);
 }
 
 
@@ -1881,11 +1951,18 @@ void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s) {
         return;
     }
     if (variant == 9) {
-        launch8p<EPI_F32, true>(g, s);
+        launch8p<EPI_F32, 1>(g, s);
         return;
     }
     if (variant == 10) {
         launch8p<EPI_F16_GELU>(g, s);
+        return;
+    }
+    if (variant >= 12 && variant <= 15) {  // debug: accumulators not transposed (fp16, GELU, fp32) / fp32
+        if (variant == 12) launch8p<EPI_F16, 2>(g, s);
+        else if (variant == 13) launch8p<EPI_F16_GELU, 2>(g, s);
+        else if (variant == 14) launch8p<EPI_F32, 2>(g, s);
+        else launch8p<EPI_F32>(g, s);
         return;
     }
     if (variant == 4 || (variant == 0 && big && !two_phase)) {

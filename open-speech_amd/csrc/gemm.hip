@@ -698,6 +698,11 @@ template <int EPI, int DBG>
 __device__ __forceinline__ void gemm8p_tile(const GemmArgs& g, int bid, h16* smem, int tid, bool pre0 = false,
                                             int next_bid = -1) {
     const int wave = tid >> 6, lane = tid & 63;
+    // transposed accumulators for the fp16 epilogues only: the fp32 and head-major forms
+    // need 217-219 VGPRs transposed (213-216 plain), which rounds the allocation up to 224
+    // and leaves 64 instead of 80 VGPRs per SIMD, too few for a 74-VGPR decoder
+    // cross-attention wave of another lane to sit beside the encoder workgroup (§5.3.1)
+    constexpr bool TR = DBG != 2 && (EPI == EPI_F16 || EPI == EPI_F16_GELU);
     int m0, n0;
     tile8p_origin(g, bid, m0, n0);
 
@@ -754,7 +759,7 @@ __device__ __forceinline__ void gemm8p_tile(const GemmArgs& g, int bid, h16* sme
 #pragma unroll
             for (int nt = 0; nt < 2; ++nt) {
                 f32x4 c = acc[a * 4 + mt][b * 2 + nt];
-                if constexpr (DBG != 2) {  // transposed: Cᵀ = W Aᵀ, the same products in the same K order
+                if constexpr (TR) {  // transposed: Cᵀ = W Aᵀ, the same products in the same K order
                     c = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[nt][0], af[mt][0], c, 0, 0, 0);
                     c = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[nt][1], af[mt][1], c, 0, 0, 0);
                 } else {
@@ -831,7 +836,7 @@ __device__ __forceinline__ void gemm8p_tile(const GemmArgs& g, int bid, h16* sme
             for (int i = 0; i < 2; ++i)
                 __builtin_amdgcn_global_load_lds((const void*)src8p(g, nm0, nn0, H, i, wave, lane),
                                                  (OSW_LDS void*)(smem + H * HT + (i * 8 + wave) * 8 * BK), 16, 0, 0);
-        if constexpr (DBG != 1) staged_epilogue_next0<EPI, DBG != 2>(g, acc, m0, n0, wm, wn, (char*)smem, tid);
+        if constexpr (DBG != 1) staged_epilogue_next0<EPI, TR>(g, acc, m0, n0, wm, wn, (char*)smem, tid);
         return;
     }
     if constexpr (DBG == 1) {
@@ -842,7 +847,7 @@ __device__ __forceinline__ void gemm8p_tile(const GemmArgs& g, int bid, h16* sme
             for (int j = 0; j < 4; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
         if (t == 1234.5f) ((float*)g.C)[tid] = t;  // keeps the loop live
     } else {
-        staged_epilogue<EPI, true, DBG != 2>(g, acc, m0, n0, wm, wn, (char*)smem, tid);
+        staged_epilogue<EPI, true, TR>(g, acc, m0, n0, wm, wn, (char*)smem, tid);
     }
 }
 
@@ -1966,9 +1971,13 @@ void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s) {
         return;
     }
     if (variant == 4 || (variant == 0 && big && !two_phase)) {
+        static const bool plain = [] {  // OSW_GEMM_TR=0: fp16 epilogues without transposed accumulators (A/B)
+            const char* e = std::getenv("OSW_GEMM_TR");
+            return e && e[0] == '0';
+        }();
         switch (g.epi) {
-            case EPI_F16: launch8p<EPI_F16>(g, s); return;
-            case EPI_F16_GELU: launch8p<EPI_F16_GELU>(g, s); return;
+            case EPI_F16: plain ? launch8p<EPI_F16, 2>(g, s) : launch8p<EPI_F16>(g, s); return;
+            case EPI_F16_GELU: plain ? launch8p<EPI_F16_GELU, 2>(g, s) : launch8p<EPI_F16_GELU>(g, s); return;
             case EPI_F32_RESID: launch8p<EPI_F32_RESID>(g, s); return;
             case EPI_F32_GELU_POS: launch8p<EPI_F32_GELU_POS>(g, s); return;
             case EPI_F32: launch8p<EPI_F32>(g, s); return;

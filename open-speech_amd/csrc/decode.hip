@@ -542,10 +542,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
 // operation, so the output is bit-identical; what goes away is the device-scope partial
 // stores, the arrival ticket and the last arriver's second round trip, which cost 8 of
 // the chunk kernel's 81 us at 64 windows (tools/probe/xattn_probe.hip: 72 us without
-// them, 71 us for a plain stream of the same bytes).  PF: the next chunk's K/V loads go
-// out before the current chunk's arithmetic (two register sets).
-template <bool PF>
-__global__ __launch_bounds__(256) void dec_xattn_pair_kernel(const float* __restrict__ part, int ks,
+// them, 71 us for a plain stream of the same bytes).  PF 1: the next chunk's K/V loads go
+// out before the current chunk's arithmetic (two register sets, 126 VGPRs).  PF 0: no
+// prefetch, capped at 80 VGPRs (6 waves per SIMD; 77 used, no spills), so a wave fits
+// beside an encoder GEMM workgroup of another lane (§5.3.1).  (Loading the next chunk's K
+// as soon as the scores are done and its V after P·V, in one register set, needs 107
+// VGPRs; capped at 80 it spills 103.)
+template <int PF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF == 1 ? 1 : 6))) void dec_xattn_pair_kernel(const float* __restrict__ part, int ks,
                                                              const float* __restrict__ bias,
                                                              const h16* __restrict__ xk, const h16* __restrict__ xv,
                                                              int H, int W, int T, h16* __restrict__ out,
@@ -571,7 +575,7 @@ __global__ __launch_bounds__(256) void dec_xattn_pair_kernel(const float* __rest
             vf[u] = __builtin_nontemporal_load((const h16x8*)(xv + hoff + (int64_t)key * HD + 8 * c));
         }
     };
-    h16x8 kf[PF ? 2 : 1][XU], vf[PF ? 2 : 1][XU];
+    h16x8 kf[PF == 1 ? 2 : 1][XU], vf[PF == 1 ? 2 : 1][XU];
     load(0, kf[0], vf[0]);
     {
         const int64_t slab = (int64_t)W * D;
@@ -594,9 +598,9 @@ __global__ __launch_bounds__(256) void dec_xattn_pair_kernel(const float* __rest
     for (int i = 0; i < 8; ++i) q[i] = qsh[8 * c + i];
 #pragma unroll
     for (int chunk = 0; chunk < XCH; ++chunk) {
-        const int cur = PF ? (chunk & 1) : 0;
-        if (!PF && chunk > 0) load(chunk, kf[0], vf[0]);
-        if (PF && chunk + 1 < XCH) load(chunk + 1, kf[cur ^ 1], vf[cur ^ 1]);
+        const int cur = PF == 1 ? (chunk & 1) : 0;
+        if (PF == 0 && chunk > 0) load(chunk, kf[0], vf[0]);
+        if (PF == 1 && chunk + 1 < XCH) load(chunk + 1, kf[cur ^ 1], vf[cur ^ 1]);
         const int k0 = chunk * per, nk = min(T, k0 + per) - k0;
         float sc[XU], mx = -INFINITY;
 #pragma unroll
@@ -1515,8 +1519,8 @@ void launch_dec_cross_attn(const float* part, int ks, const float* bias, const h
     static const bool pair_on = std::getenv("OSW_XATTN_PAIR") && std::getenv("OSW_XATTN_PAIR")[0] == '1';
     static const bool pair_pf = !std::getenv("OSW_XATTN_PAIR_PF") || std::getenv("OSW_XATTN_PAIR_PF")[0] != '0';
     if (beam == 1 && pair_on && W * H >= 768) {
-        if (pair_pf) dec_xattn_pair_kernel<true><<<W * H, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, out, lo_off, st);
-        else dec_xattn_pair_kernel<false><<<W * H, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, out, lo_off, st);
+        if (pair_pf) dec_xattn_pair_kernel<1><<<W * H, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, out, lo_off, st);
+        else dec_xattn_pair_kernel<0><<<W * H, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, out, lo_off, st);
         return;
     }
     switch (beam) {

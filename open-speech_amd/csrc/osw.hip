@@ -651,7 +651,8 @@ bool skinny_ok(const GemmArgs& g) {
     // very wide N (logits) at >= 24 rows: the 128x128 LDS-tiled kernel streams the
     // weights faster (measured 36 vs 44 us at M = 64, N = 51866)
     // (32-row skinny groups for the 64-row logits, which would fit beside another lane's
-    // encoder workgroup: 4707 vs 4789 audio-s/s, measured)
+    // encoder workgroup: 4707 vs 4789 audio-s/s, measured; again with the fragment-major
+    // weights in round 4: 5020 / 5019 vs 5065 / 5048, gpurun_out/r04_ag)
     if (g.N >= 16384 && g.M >= 24) return false;
     return g.M <= 64 && g.K % 128 == 0 &&
            (g.epi == EPI_F16 || g.epi == EPI_F16_GELU || g.epi == EPI_F32_RESID || g.epi == EPI_F32);

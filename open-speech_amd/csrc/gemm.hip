@@ -302,9 +302,9 @@ __device__ __forceinline__ int acc_col(int wn, int ni) { return IL ? (ni >> 1) *
 // Output rows leave through nontemporal stores: the encoder's activations (0.5-2 GB per
 // GEMM at 64 windows) stream past the MALL instead of evicting the weights and the
 // next GEMM's operand panels (8p GEMMs 4-7 % and the attention after them 6 % faster).
-// TR (8-phase kernel, IL): the accumulators are transposed (the kernel swaps the MFMA
-// operands), lane l of block (mi, ni) holding C[row + (l & 15)][col + 4 (l >> 4) + e], so the
-// image takes one 8-B (fp16) / 16-B (fp32) write per block instead of four 2-B / 4-B ones
+// TR (8-phase kernel, IL, fp16 epilogues): the accumulators are transposed (the kernel swaps
+// the MFMA operands), lane l of block (mi, ni) holding C[row + (l & 15)][col + 4 (l >> 4) + e],
+// so the image takes one 8-B write per block instead of four 2-B ones
 // (fc1 at 64 windows 1488 -> 1432 us, + GELU 1694 -> 1627 us; profiles/r04_s_epilogue.jsonl, r04_t_epilogue_forms.jsonl)
 template <int EPI, bool IL = false, bool TR = false>
 __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], int m0, int n0, int wm,
@@ -369,21 +369,7 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
     } else {
         float* T = (float*)smem;
         for (int half = 0; half < 2; ++half) {
-            if (TR && IL) {
-#pragma unroll
-                for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-                    for (int ni = 0; ni < 4; ++ni) {
-                        if ((mi >> 2) != half) continue;
-                        const int row = acc_row<IL>(wm, mi) - half * 128 + (lane & 15);
-                        const int col = acc_col<IL>(wn, ni) + 4 * (lane >> 4);
-                        const int n = min(n0 + col, g.N - 4);
-                        f32x4 v;
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) v[e] = epi_value<EPI>(g, m0 + half * 128 + row, n + e, acc[mi][ni][e]);
-                        *(f32x4*)&T[ep32(row, col)] = v;
-                    }
-            } else if (IL || wm == half) {
+            if (IL || wm == half) {
 #pragma unroll
                 for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
@@ -641,21 +627,7 @@ __device__ __forceinline__ void staged_epilogue_next0(const GemmArgs& g, f32x4 (
         } else {
             float* T = (float*)(smem + 4 * HT * 2);
             // pass p = rows [64 p, 64 p + 64): wave rows (mi >> 2) * 128 + wm * 64
-            if (TR && wm == (pass & 1)) {
-#pragma unroll
-                for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-                    for (int ni = 0; ni < 4; ++ni) {
-                        if ((mi >> 2) != (pass >> 1)) continue;
-                        const int row = acc_row<true>(wm, mi) - pass * PR + (lane & 15);
-                        const int col = acc_col<true>(wn, ni) + 4 * (lane >> 4);
-                        const int n = min(n0 + col, g.N - 4);
-                        f32x4 v;
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) v[e] = epi_value<EPI>(g, m0 + pass * PR + row, n + e, acc[mi][ni][e]);
-                        *(f32x4*)&T[ep32(row, col)] = v;
-                    }
-            } else if (wm == (pass & 1)) {
+            if (wm == (pass & 1)) {
 #pragma unroll
                 for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
@@ -860,7 +832,7 @@ __device__ __forceinline__ void gemm8p_tile(const GemmArgs& g, int bid, h16* sme
 // then fit beside an encoder workgroup (<= 30 KiB of LDS, <= 80 VGPRs); the 64-row logits
 // GEMM (80 KiB) does not.  4832 vs 4789 audio-s/s (12 steps, two runs each).
 // DBG (debug variants): 1 no epilogue (9: main-loop time alone), 2 the accumulators not
-// transposed (the round-3 epilogue; 12-14)
+// transposed (the round-3 fp16 epilogues; 12, 13)
 template <int EPI, int DBG = 0>
 __global__ __launch_bounds__(GNT, 1) void gemm8p_kernel(GemmArgs g) {
     extern __shared__ __attribute__((aligned(16))) h16 smem[];  // [2][A0 A1 W0 W1][128*64]
@@ -1963,11 +1935,9 @@ void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s) {
         launch8p<EPI_F16_GELU>(g, s);
         return;
     }
-    if (variant >= 12 && variant <= 15) {  // debug: accumulators not transposed (fp16, GELU, fp32) / fp32
+    if (variant == 12 || variant == 13) {  // debug: fp16 / GELU epilogues on accumulators not transposed
         if (variant == 12) launch8p<EPI_F16, 2>(g, s);
-        else if (variant == 13) launch8p<EPI_F16_GELU, 2>(g, s);
-        else if (variant == 14) launch8p<EPI_F32, 2>(g, s);
-        else launch8p<EPI_F32>(g, s);
+        else launch8p<EPI_F16_GELU, 2>(g, s);
         return;
     }
     if (variant == 4 || (variant == 0 && big && !two_phase)) {

@@ -62,7 +62,7 @@ def test_8phase_transposed_epilogues_bit_identical(eng, M, N, K):
     """The 8-phase GEMM's fp16 epilogues run on transposed accumulators (Cᵀ = W·Aᵀ: the
     same products in the same K order): debug variants 8 / 10 (fp16, fp16 +
     GELU, transposed) equal 12 / 13 (the same epilogues on the plain accumulators) bit for
-    bit, 15 equals 14 (fp32), and the fp16 values match float64 references."""
+    bit, and the fp16 values match float64 references."""
     rng = np.random.default_rng(M * 3 + N + K)
     A = rng.uniform(-1, 1, (M, K)).astype(np.float16)
     W = rng.uniform(-1, 1, (N, K)).astype(np.float16)
@@ -72,10 +72,8 @@ def test_8phase_transposed_epilogues_bit_identical(eng, M, N, K):
 
     c8, c12 = f16(eng.debug_gemm(A, W, 8)[0]), f16(eng.debug_gemm(A, W, 12)[0])
     c10, c13 = f16(eng.debug_gemm(A, W, 10)[0]), f16(eng.debug_gemm(A, W, 13)[0])
-    c15, c14 = eng.debug_gemm(A, W, 15)[0], eng.debug_gemm(A, W, 14)[0]
     assert np.array_equal(c8, c12)
     assert np.array_equal(c10, c13)
-    assert np.array_equal(c15, c14)
     ref = A.astype(np.float64) @ W.astype(np.float64).T
     from scipy.special import erf
     gelu = 0.5 * ref * (1.0 + erf(ref / np.sqrt(2.0)))
@@ -84,4 +82,3 @@ def test_8phase_transposed_epilogues_bit_identical(eng, M, N, K):
     tol = 2e-3 * np.sqrt(K)
     assert np.abs(out - ref).max() < tol + 1e-3 * np.abs(ref).max()
     assert np.abs(outg - gelu).max() < tol + 1e-3 * np.abs(gelu).max()
-    assert np.abs(c15 - ref).max() < tol

@@ -32,6 +32,7 @@ import osw_path  # noqa: E402
 osw_path.load()
 from open_speech_amd import dims as D  # noqa: E402
 from open_speech_amd import synth  # noqa: E402
+from open_speech_amd.distributed import REFILL_MIN  # noqa: E402
 from open_speech_amd.engine import DecodeConfig, WhisperEngine  # noqa: E402
 from open_speech_amd.tokenizer import WhisperTokenizer, get_suppressed_tokens  # noqa: E402
 
@@ -67,7 +68,7 @@ def parse(argv=None):
                     help="BASELINE configs[4]: concurrent /v1/audio/stream sessions simulated through the backend "
                          "(0 = skip)")
     ap.add_argument("--stream-speech-s", type=float, default=6.0, help="seconds of speech per streaming session")
-    ap.add_argument("--refill-min", type=int, default=24,
+    ap.add_argument("--refill-min", type=int, default=REFILL_MIN,
                     help="row refill (realistic lengths): admit queued clips once this many rows are free")
     ap.add_argument("--realistic-steps", type=int, default=9,
                     help="also time this many steps with realistic output lengths (random weights never emit "

@@ -147,12 +147,6 @@ int osw_create_sibling(osw_ctx* parent, int32_t max_batch, osw_ctx** out);
  * it, so small streaming encoders of sibling lanes run side by side.  Default 9
  * (OSW_BATON_MIN_WINDOWS); 0 = every encoder takes the baton.  Per context. */
 int osw_set_encoder_baton_min(osw_ctx* ctx, int32_t min_windows);
-/* Which cross-attention form a greedy decoder step of `rows` windows (one row each, all
- * of the last encode) takes: 0 = per-head cross K/V (the encoder's crosskv GEMM output),
- * 1 = the E-form (attention over the encoder output itself, q' = Wk_h^T q_h / 8 and the
- * V projection after the softmax).  -1 on a null ctx.  Both forms give
- * the reference's result; the E-form never rounds K/V to fp16. */
-int osw_cross_attention_form(osw_ctx* ctx, int32_t rows);
 
 /* Upload one canonical tensor (names and dtypes: open-speech_amd/weights.py). */
 int osw_set_weight(osw_ctx* ctx, const char* name, const void* host, int64_t nbytes);

@@ -83,7 +83,6 @@ _SIGS = {
     "osw_debug_gemm": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
                                  P(C.c_float), C.c_int32, P(C.c_float)]),
     "osw_set_encoder_baton_min": (C.c_int, [C.c_void_p, C.c_int32]),
-    "osw_cross_attention_form": (C.c_int, [C.c_void_p, C.c_int32]),
     "osw_set_profiling": (C.c_int, [C.c_void_p, C.c_int32]),
     "osw_get_profile": (C.c_int, [C.c_void_p, P(osw_profile)]),
     "osw_stream": (C.c_void_p, [C.c_void_p]),

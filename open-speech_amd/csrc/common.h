@@ -143,9 +143,6 @@ struct GemmArgs {
     // MFMA B fragment of one k32 step is 1 KB contiguous, so a wave's weight load is one
     // coalesced 1-KB piece instead of 16 rows x 64 B; launch_frag_pack), or nullptr
     const h16* Wf;
-    // skinny kernel: A of the 64-column block bx starts at A + bx * a_col_stride (the V
-    // projection of the E-form cross-attention: one head's normalised P·E per block)
-    int64_t a_col_stride;
 };
 
 // fp32 -> (hi, lo) fp16 pair: hi = fp16(v), lo = fp16(v - hi)

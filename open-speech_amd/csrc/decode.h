@@ -58,18 +58,6 @@ constexpr int MAX_BEAM = 8;
 constexpr int XPART = 72;     // floats per (decoder row, head, key chunk) cross-attention partial: m, l, pad, acc[64]
 constexpr int XCHUNKS = 8;    // fixed key chunks per (window, head) in cross-attention
 constexpr int SEL_SPLIT = 16;  // vocabulary slices per row in the selection kernels
-constexpr int EX_CHUNKS = 4;   // key chunks per window of the E-form cross-attention (exattn.hip)
-constexpr int EX_HP = 32;        // E-form heads padded to one 32-wide MFMA tile (q' rows per window)
-constexpr int EX_MIN_ROWS = 24;
-constexpr bool kEformDefault = false;  // E-form on unless OSW_EFORM=0 (osw_cross_attention_form)  // greedy decoder batches from this many windows use the E-form
-
-// E-form cross-attention (exattn.hip): see the header of that file
-bool exattn_supported(int D, int H);
-void launch_ex_pack_kT(const h16* W, int L, int D, h16* kT, hipStream_t s);
-void launch_ex_qk(const float* part, int ks, const float* bias, int rows, int D, const h16* kT, h16* qp, int64_t qlo,
-                  hipStream_t s);
-void launch_exattn(const h16* E, const h16* qp, int64_t qlo, int W, int T, int D, float* ws, int pstride, h16* pen,
-                   int64_t pen_lo, const SelState* st, hipStream_t s);
 
 void launch_refill_rows(const int* pack, int k, int P, int* prompt, int* budget, int* cur_tok, int* pos, SelState* st,
                         hipStream_t s);

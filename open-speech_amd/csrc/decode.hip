@@ -535,142 +535,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
     xattn_merge(ws, r0, beam, H, h, out, lo_off);
 }
 
-// Greedy rows when there are enough (window, head) pairs to fill the chip: one workgroup
-// per pair walks the pair's 8 key chunks itself and merges their partials from LDS.  The
-// per-chunk arithmetic (q reduction, scores, chunk max, exp, P·V, the cross-wave sums) and
-// the fixed-order merge are dec_xattn_chunk_kernel<1>'s and xattn_merge's, operation for
-// operation, so the output is bit-identical; what goes away is the device-scope partial
-// stores, the arrival ticket and the last arriver's second round trip, which cost 8 of
-// the chunk kernel's 81 us at 64 windows (tools/probe/xattn_probe.hip: 72 us without
-// them, 71 us for a plain stream of the same bytes).  PF 1: the next chunk's K/V loads go
-// out before the current chunk's arithmetic (two register sets, 126 VGPRs).  PF 0: no
-// prefetch, capped at 80 VGPRs (6 waves per SIMD; 77 used, no spills), so a wave fits
-// beside an encoder GEMM workgroup of another lane (§5.3.1).  (Loading the next chunk's K
-// as soon as the scores are done and its V after P·V, in one register set, needs 107
-// VGPRs; capped at 80 it spills 103.)
-template <int PF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF == 1 ? 1 : 6))) void dec_xattn_pair_kernel(const float* __restrict__ part, int ks,
-                                                             const float* __restrict__ bias,
-                                                             const h16* __restrict__ xk, const h16* __restrict__ xv,
-                                                             int H, int W, int T, h16* __restrict__ out,
-                                                             int64_t lo_off, const SelState* __restrict__ st) {
-    __shared__ float red[4][HD];
-    __shared__ float rm[4], rl[4];
-    __shared__ float qsh[HD];
-    __shared__ float pm[XCH], pl[XCH], pacc[XCH][HD];
-    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, kg = tid >> 3, c = tid & 7;
-    const int p = blockIdx.x;
-    if (p >= W * H) return;
-    const int h = p % H, w = p / H;
-    if (st[w].done) return;
-    const int D = H * HD;
-    const int per = (T + XCH - 1) / XCH;
-    const int64_t hoff = ((int64_t)w * H + h) * T * HD;
-    auto load = [&](int chunk, h16x8 (&kf)[XU], h16x8 (&vf)[XU]) {
-        const int k0 = chunk * per, nk = min(T, k0 + per) - k0;
-#pragma unroll
-        for (int u = 0; u < XU; ++u) {
-            const int key = k0 + min(u * 32 + kg, nk - 1);
-            kf[u] = __builtin_nontemporal_load((const h16x8*)(xk + hoff + (int64_t)key * HD + 8 * c));
-            vf[u] = __builtin_nontemporal_load((const h16x8*)(xv + hoff + (int64_t)key * HD + 8 * c));
-        }
-    };
-    h16x8 kf[PF == 1 ? 2 : 1][XU], vf[PF == 1 ? 2 : 1][XU];
-    load(0, kf[0], vf[0]);
-    {
-        const int64_t slab = (int64_t)W * D;
-        const int64_t off = (int64_t)w * D + h * HD + lane;
-        float v = 0.f;
-        int s = wv;
-        for (; s + 4 < ks; s += 8) v += part[s * slab + off] + part[(s + 4) * slab + off];
-        if (s < ks) v += part[s * slab + off];
-        red[wv][lane] = v;
-    }
-    lds_barrier();
-    if (wv == 0) {
-        float r = bias[h * HD + lane];
-        r += red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-        qsh[lane] = (float)(h16)r * 0.125f;
-    }
-    lds_barrier();
-    float q[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) q[i] = qsh[8 * c + i];
-#pragma unroll
-    for (int chunk = 0; chunk < XCH; ++chunk) {
-        const int cur = PF == 1 ? (chunk & 1) : 0;
-        if (PF == 0 && chunk > 0) load(chunk, kf[0], vf[0]);
-        if (PF == 1 && chunk + 1 < XCH) load(chunk + 1, kf[cur ^ 1], vf[cur ^ 1]);
-        const int k0 = chunk * per, nk = min(T, k0 + per) - k0;
-        float sc[XU], mx = -INFINITY;
-#pragma unroll
-        for (int u = 0; u < XU; ++u) {
-            float d = 0.f;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) d = fmaf((float)kf[cur][u][i], q[i], d);
-            d += xor_lane<1>(d);
-            d += xor_lane<2>(d);
-            d += xor_lane<4>(d);
-            sc[u] = d;
-            if (u * 32 + kg < nk) mx = fmaxf(mx, d);
-        }
-        mx = wave_max(mx);
-        if (lane == 0) rm[wv] = mx;
-        lds_barrier();
-        const float m = fmaxf(fmaxf(rm[0], rm[1]), fmaxf(rm[2], rm[3]));
-        float acc[8], ls = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] = 0.f;
-#pragma unroll
-        for (int u = 0; u < XU; ++u) {
-            const float pu = u * 32 + kg < nk ? __expf(sc[u] - m) : 0.f;
-            ls += pu;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) acc[e] = fmaf(pu, (float)vf[cur][u][e], acc[e]);
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            float a = acc[e];
-            a += xor_lane<8>(a);
-            a += xor_lane<16>(a);
-            a += xor_lane<32>(a);
-            acc[e] = a;
-        }
-        if (lane < 8) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) red[wv][8 * c + e] = acc[e];
-        }
-        float l = c == 0 ? ls : 0.f;
-        l = wave_sum(l);
-        if (lane == 0) rl[wv] = l;
-        lds_barrier();
-        if (wv == 0) {
-            pacc[chunk][lane] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
-            if (lane == 0) {
-                pm[chunk] = m;
-                pl[chunk] = (rl[0] + rl[1]) + (rl[2] + rl[3]);
-            }
-        }
-        lds_barrier();  // red, rm, rl are the next chunk's
-    }
-    if (wv != 0) return;
-    float mm[XCH];
-    float M = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < XCH; ++i) {
-        mm[i] = pm[i];
-        M = fmaxf(M, mm[i]);
-    }
-    float L = 0.f, O = 0.f;
-#pragma unroll
-    for (int i = 0; i < XCH; ++i) {
-        const float e = __expf(mm[i] - M);
-        L = fmaf(pl[i], e, L);
-        O = fmaf(pacc[i][lane], e, O);
-    }
-    split_h16(O / L, out, out + lo_off, (int64_t)w * D + h * HD + lane);
-}
-
 // Beam rows (2..8 per window): dec_xattn_chunk_kernel's (window, head, key chunk)
 // decomposition, partials and last-arriver merge, with the scores and P·V on MFMA (the
 // VALU form ran VALU-bound: 120 us per launch at 64 windows x 5 beams against 84 us for
@@ -914,23 +778,6 @@ __global__ __launch_bounds__(256) void dec_reduce_gelu_kernel(const float* __res
                                                               h16* __restrict__ y, int64_t lo_off) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x)
         split_h16(gelu_reduce_one(part, ks, total, bias, i, (int)(i % N)), y, y + lo_off, i);
-}
-
-// the E-form V projection's split-K reduce: y = bias + Σ_k part[k] (k in order) as an hi/lo pair
-__global__ __launch_bounds__(256) void dec_reduce_kernel(const float* __restrict__ part, int ks, int64_t total, int N,
-                                                         const float* __restrict__ bias, h16* __restrict__ y,
-                                                         int64_t lo_off) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        float p[8];
-        float v = 0.f;
-        for (int k0 = 0; k0 < ks; k0 += 8) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) p[j] = part[(int64_t)min(k0 + j, ks - 1) * total + i];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v += k0 + j < ks ? p[j] : 0.f;
-        }
-        split_h16(bias[(int)(i % N)] + v, y, y + lo_off, i);
-    }
 }
 
 #include "select.h"
@@ -1510,19 +1357,6 @@ void launch_dec_cross_attn(const float* part, int ks, const float* bias, const h
         }
         return;
     }
-    // OSW_XATTN_PAIR=1 (one row per window, >= 768 (window, head) pairs): one workgroup per
-    // pair walking its 8 chunks, bit-identical to the chunk kernel.  Alone it is faster (74.1
-    // vs 80.4 us at 64 windows, 43.1 vs 43.2 at 32; tools/probe/xattn_probe.hip), but beside
-    // sibling lanes' encoders it is not: 126 VGPRs (84 without the prefetch) do not fit next
-    // to an encoder workgroup, and the 3-lane headline measured 4911 / 4904 (4839 / 4842
-    // without the prefetch) against 4922 / 4914 audio-s/s for the chunk kernel (r04_j).
-    static const bool pair_on = std::getenv("OSW_XATTN_PAIR") && std::getenv("OSW_XATTN_PAIR")[0] == '1';
-    static const bool pair_pf = !std::getenv("OSW_XATTN_PAIR_PF") || std::getenv("OSW_XATTN_PAIR_PF")[0] != '0';
-    if (beam == 1 && pair_on && W * H >= 768) {
-        if (pair_pf) dec_xattn_pair_kernel<1><<<W * H, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, out, lo_off, st);
-        else dec_xattn_pair_kernel<0><<<W * H, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, out, lo_off, st);
-        return;
-    }
     switch (beam) {
         case 1: dec_xattn_chunk_kernel<1><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off, st); break;
         case 2: dec_xattn_chunk_kernel<2><<<grid, 256, 0, s>>>(part, ks, bias, xk, xv, H, W, T, beam, ws, ticket, out, lo_off, st); break;
@@ -1538,13 +1372,6 @@ void launch_dec_resid_ln(const float* part, int ks, int B, int D, const float* b
                          const int* tok, const int* pos, int ctx, int V, hipStream_t s, int pos_row) {
     ResLnArgs A{part, ks, (int64_t)B * D, bias, x, x, g, be, tok_emb, pos_emb, tok, pos, ctx, D, V, pos_row};
     dec_resid_ln_kernel<<<B, 256, 0, s>>>(A, y, lo_off);
-}
-
-void launch_dec_reduce(const float* part, int ks, int B, int N, const float* bias, h16* y, int64_t lo_off,
-                       hipStream_t s) {
-    const int64_t total = (int64_t)B * N;
-    dec_reduce_kernel<<<(unsigned)std::min<int64_t>((total + 255) / 256, 1024), 256, 0, s>>>(part, ks, total, N, bias,
-                                                                                            y, lo_off);
 }
 
 void launch_dec_reduce_gelu(const float* part, int ks, int B, int N, const float* bias, h16* y, int64_t lo_off,

@@ -1339,9 +1339,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL ? 4 : 1
         const int row = RPP * j + lane / CPR;
         acl[i] = ((lane % CPR) ^ (row & SWM)) * 8;
         const int64_t gr = min(mb + row, g.M - 1);
-        const int64_t acol = (int64_t)bx * g.a_col_stride;
-        asrc[0][i] = grp_row(g.A, gr, g.a_grp_rows, g.a_grp_stride, g.lda) + acol + k0;
-        if constexpr (LO) asrc[NIMG - 1][i] = grp_row(g.A_lo, gr, g.a_grp_rows, g.a_grp_stride, g.lda) + acol + k0;
+        asrc[0][i] = grp_row(g.A, gr, g.a_grp_rows, g.a_grp_stride, g.lda) + k0;
+        if constexpr (LO) asrc[NIMG - 1][i] = grp_row(g.A_lo, gr, g.a_grp_rows, g.a_grp_stride, g.lda) + k0;
     }
     auto stageA = [&](int buf, int c) {
         if constexpr (PRO != PRO_NONE) return;

@@ -43,7 +43,6 @@ void launch_dec_cross_attn(const float*, int, const float*, const h16*, const h1
 void launch_dec_resid_ln(const float*, int, int, int, const float*, float*, const float*, const float*, h16*, int64_t,
                          const h16*, const float*, const int*, const int*, int, int, hipStream_t, int pos_row = 0);
 void launch_dec_reduce_gelu(const float*, int, int, int, const float*, h16*, int64_t, hipStream_t);
-void launch_dec_reduce(const float*, int, int, int, const float*, h16*, int64_t, hipStream_t);
 void launch_ingest_sumsq(const int16_t*, int, int, const int2*, int, float*, float*, hipStream_t);
 void launch_ingest_gain(const int16_t*, int64_t, int, int, float, int16_t*, hipStream_t);
 void launch_ingest_resample(const int16_t*, int64_t, const float*, int, int, int, int64_t, int64_t, int16_t*,
@@ -238,15 +237,6 @@ struct osw_ctx {
     int* budget = nullptr;     // per-row token budgets (osw_decode_opts::token_budget)
     unsigned long long* seed_d = nullptr;  // sampling seed of the current decode call
     int64_t part_floats = 0;
-    // E-form cross-attention (exattn.hip; greedy batches of EX_MIN_ROWS.. windows): q' of every
-    // row and head as hi/lo fp16 [2][B][HP][D] (heads past H stay zero), the per-chunk
-    // partials [B][EX_CHUNKS][H][D + 8] and the merged, normalised P·E [2][B][H][D]
-    bool eform = false;
-    h16* exq = nullptr;
-    int64_t exq_lo = 0;
-    float* exws = nullptr;
-    h16* pen = nullptr;
-    int64_t pen_lo = 0;
 
     // decode-step graphs (CH steps per replay), one per key (batch rows, prompt length,
     // decode options); a small LRU so a serving mix of batch sizes replays instead of
@@ -409,17 +399,6 @@ void build_weight_table(osw_ctx* c) {
         c->w[n + ".frag"].set = true;  // derived: written by pack_frag
     };
     frag("dec.tok", d.n_vocab, Dd);
-    frag("dec.crosskv.w", L * 2 * Dd, De);  // the E-form V projection streams its V rows
-    // E-form cross-attention (exattn.hip, OSW_EFORM=1): every layer's Wk as [H][D][64],
-    // derived from dec.crosskv.w like the fragment-major copies (+ 13 MB at turbo); only in
-    // contexts created with the E-form on (siblings share the parent's table)
-    {
-        const char* ef = getenv("OSW_EFORM");
-        if ((ef ? atoi(ef) != 0 : kEformDefault) && Dd == De) {
-            add_tensor(c, "dec.crosskv.kT", L * Dd * De, true);
-            c->w["dec.crosskv.kT"].set = true;
-        }
-    }
     for (int i = 0; i < d.n_text_layer; ++i) {
         const std::string p = "dec.l" + std::to_string(i);
         frag(p + ".qkv.w", 3 * Dd, Dd);
@@ -470,11 +449,6 @@ const h16* WFR(osw_ctx* c, const std::string& n) {
 // rewrite the fragment-major copy after the matrix was written (on the context's stream)
 void pack_frag(osw_ctx* c, const std::string& n) {
     const Tensor& t = W(c, n);
-    if (n == "dec.crosskv.w" && c->w.count("dec.crosskv.kT")) {
-        launch_ex_pack_kT((const h16*)t.ptr, c->d.n_text_layer, c->d.n_text_state, (h16*)W(c, "dec.crosskv.kT").ptr,
-                          c->stream);
-        HIPCHK(hipGetLastError());
-    }
     if (!t.frag_n) return;
     launch_frag_pack((const h16*)t.ptr, t.frag_k, t.frag_n, t.frag_k, (h16*)W(c, n + ".frag").ptr, c->stream);
     HIPCHK(hipGetLastError());
@@ -605,22 +579,6 @@ void setup_workspace(osw_ctx* c) {
         for (auto& nk : shapes)
             if (nk[0] != d.n_vocab) p2 = std::max<int64_t>(p2, (int64_t)skinny_ksplit((int)nk[0], (int)nk[1]) * nk[0]);
         c->part2 = dalloc<float>(p2 * std::min<int64_t>(R, GELU_ROWS), o);
-    }
-    {
-        const int D = (int)Dd, H = d.n_text_head;
-        // OSW_EFORM=0/1 overrides the default (read per context, so tests can hold both forms)
-        const char* ef = getenv("OSW_EFORM");
-        const bool off = ef ? atoi(ef) == 0 : !kEformDefault;
-        c->eform = !off && De == Dd && exattn_supported(D, H) && c->w.count("dec.crosskv.kT");
-        if (c->eform) {
-            const int64_t HP = EX_HP, BE = std::min<int64_t>(B, 128);
-            c->exq_lo = BE * HP * D;
-            c->exq = dalloc<h16>(2 * c->exq_lo, o);
-            HIPCHK(hipMemset(c->exq, 0, (size_t)2 * c->exq_lo * sizeof(h16)));  // padded heads stay zero
-            c->exws = dalloc<float>(BE * EX_CHUNKS * H * (int64_t)(D + 8), o);
-            c->pen_lo = BE * H * (int64_t)D;
-            c->pen = dalloc<h16>(2 * c->pen_lo, o);
-        }
     }
     HIPCHK(hipHostMalloc((void**)&c->done_host, sizeof(int), 0));
 }
@@ -911,9 +869,6 @@ bool decoder_step(osw_ctx* c, int nb, int group, bool gather, const SelFuse* sf 
         decoder_step_fused(c, nb, group, gather, nb == 1 ? sf : nullptr);
         return sf != nullptr && nb == 1;
     }
-    // greedy batches of EX_MIN_ROWS.. windows: the E-form cross-attention (exattn.hip)
-    const bool eform = c->eform && !c->row_pos && group == 1 && !gather && nb >= EX_MIN_ROWS && nb <= 128 &&
-                       nb == c->n_encoded;
     static const bool no_gelu_pro = getenv("OSW_NO_GELU_PRO") != nullptr;  // A/B switch
     const bool gelu_pro = nb <= GELU_ROWS && !no_gelu_pro && 4 * D / skinny_ksplit(D, 4 * D) <= GELU_KC;
     // x = tok_emb[tok] + pos_emb[pos]; xdn = LN1_0(x)
@@ -928,27 +883,7 @@ bool decoder_step(osw_ctx* c, int nb, int group, bool gather, const SelFuse* sf 
         launch_dec_resid_ln(c->part, ks, nb, D, WF(c, p + ".o.b"), c->xd, WF(c, p + ".ln2.g"), WF(c, p + ".ln2.b"),
                             c->xdn, lo_d, nullptr, nullptr, nullptr, nullptr, ctx, d.n_vocab, c->stream);
         ks = partial(c->xdn, D, p + ".xq.w", D, D);
-        if (eform) {
-            // E-form (exattn.hip): q' = Wk_h^T q_h / 8, one pass over E for all heads, the
-            // chunk merge, then the V projection (per-head A blocks) and its reduce (+ bv)
-            launch_ex_qk(c->part, ks, WF(c, p + ".xq.b"), nb, D,
-                         WH(c, "dec.crosskv.kT") + (int64_t)l * D * d.n_audio_state, c->exq, c->exq_lo, c->stream);
-            {
-                Timed t(c, CL_XATTN, 2.0 * nb * (double)T_ENC * D);
-                launch_exattn(c->E, c->exq, c->exq_lo, nb, T_ENC, D, c->exws, D + 8, c->pen, c->pen_lo, c->sel,
-                              c->stream);
-            }
-            const int64_t vrow = (int64_t)(2 * l + 1) * D;  // this layer's V rows of dec.crosskv.w
-            GemmArgs gv = gemm_plain(c->pen, (int64_t)H * D, WH(c, "dec.crosskv.w") + vrow * d.n_audio_state, nullptr,
-                                     nb, D, d.n_audio_state, nullptr, 0, EPI_F32);
-            const h16* cf = WFR(c, "dec.crosskv.w");
-            gv.Wf = cf ? cf + (vrow / 16) * (d.n_audio_state / 32) * 512 : nullptr;
-            gv.A_lo = c->pen + c->pen_lo;
-            gv.a_col_stride = d.n_audio_state;  // column block h = head h: A = its P·E row
-            REQUIRE((int64_t)skinny_ksplit(D, d.n_audio_state) * nb * D <= c->part_floats, "split-K workspace too small");
-            const int ksv = launch_gemm_skinny_partial(gv, c->part, c->stream);
-            launch_dec_reduce(c->part, ksv, nb, D, WF(c, "dec.crosskv.b") + vrow, c->dattn, lo_d, c->stream);
-        } else {
+        {
             Timed t(c, CL_XATTN, 2.0 * nb * H * (double)T_ENC * 64 * 2);
             launch_dec_cross_attn(c->part, ks, WF(c, p + ".xq.b"), c->XKV + (2 * l) * xkv_which,
                                   c->XKV + (2 * l + 1) * xkv_which, nb, H, T_ENC, group, c->dattn, lo_d, c->xws,
@@ -1885,11 +1820,6 @@ int osw_debug_gemm(osw_ctx* c, int32_t M, int32_t N, int32_t K, int32_t variant,
         (void)hipEventDestroy(e1);
         for (void* p : tmp) (void)hipFree(p);
     });
-}
-
-int osw_cross_attention_form(osw_ctx* c, int32_t rows) {
-    if (!c) return -1;
-    return (c->eform && rows >= EX_MIN_ROWS && rows <= 128) ? 1 : 0;
 }
 
 int osw_set_encoder_baton_min(osw_ctx* c, int32_t min_windows) {

@@ -23,6 +23,9 @@ from concurrent.futures import ThreadPoolExecutor
 import numpy as np
 
 N_SAMPLES = 480000
+# row refill: admit queued clips once this many decoder rows are free (the measured best
+# of 8 / 24 / 40 / 64 on the realistic-length bench)
+REFILL_MIN = 24
 
 
 class DataParallelTranscriber:
@@ -110,23 +113,30 @@ class DataParallelTranscriber:
             res.append((outs, self.gather(outs)))
         return res
 
-    def run_steps_refill(self, all_pcm, k: int, refill_min: int = 8):
+    def run_steps_refill(self, all_pcm, k: int, refill_min: int = REFILL_MIN):
         """k steps' clips with row refill (WhisperEngine.transcribe_refill): step i goes to
         lane i % lanes as in run_steps, but each lane takes ALL of its steps' clips in one
         call, so its decoder rows stay full across the step boundaries (a finished window's
         row takes the next clip) instead of every batch waiting for its longest window.
         Greedy only.  Collectives (scatter, gather) run in step order on the calling
-        thread, as in run_steps.  Returns [(local outputs, gathered ids or None)] per step."""
+        thread, as in run_steps; a lane starts as soon as its own last shard has arrived.
+        The per-lane PCM buffers persist across calls and grow on demand.
+        Returns [(local outputs, gathered ids or None)] per step."""
         torch = self.torch
         nl = len(self.lanes)
         steps = [[i for i in range(k) if i % nl == lane] for lane in range(nl)]
-        bufs = [torch.empty((len(st) * self.B, self.S), dtype=torch.int16, device=self.device) if st else None
-                for st in steps]
-        for i in range(k):  # the scatters in step order (identical on every rank)
-            lane, j = i % nl, i // nl
-            self.scatter(all_pcm, 0)
-            bufs[lane][j * self.B:(j + 1) * self.B].copy_(self.shards[0])
-        self._sync()
+        if not hasattr(self, "_refill_bufs"):
+            self._refill_bufs = {}
+        bufs = {}
+        for lane, st in enumerate(steps):
+            if not st:
+                continue
+            need = len(st) * self.B
+            buf = self._refill_bufs.get(lane)
+            if buf is None or buf.shape[0] < need:
+                buf = torch.empty((need, self.S), dtype=torch.int16, device=self.device)
+                self._refill_bufs[lane] = buf
+            bufs[lane] = buf[:need]
         cfg = self.cfg
 
         def lane_call(lane):
@@ -141,12 +151,19 @@ class DataParallelTranscriber:
                                              refill_min=refill_min)
             return eng.transcribe_refill(list(bufs[lane].numpy()), c, refill_min=refill_min)
 
-        lanes = [lane for lane in range(nl) if steps[lane]]
-        if self.pool is None:
-            outs = {lane: lane_call(lane) for lane in lanes}
-        else:
-            futs = {lane: self.pool.submit(lane_call, lane) for lane in lanes}
-            outs = {lane: f.result() for lane, f in futs.items()}
+        futs, outs = {}, {}
+        for i in range(k):  # the scatters in step order (identical on every rank)
+            lane, j = i % nl, i // nl
+            self.scatter(all_pcm, 0)
+            bufs[lane][j * self.B:(j + 1) * self.B].copy_(self.shards[0])
+            if j == len(steps[lane]) - 1:  # this lane's last shard: start it
+                self._sync()
+                if self.pool is None:
+                    outs[lane] = lane_call(lane)
+                else:
+                    futs[lane] = self.pool.submit(lane_call, lane)
+        for lane, f in futs.items():
+            outs[lane] = f.result()
         res = []
         for i in range(k):
             lane, j = i % nl, i // nl

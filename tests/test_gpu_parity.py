@@ -127,7 +127,7 @@ def test_wide_batch_greedy_matches_fp16_oracle():
     the skinny one: 32 windows (two clips alternating) against the fp16 oracle, and every
     copy of a clip decodes identically."""
     from oracle import decode as odec
-    from oracle.model import GPU_POINTS, WhisperOracle
+    from oracle.model import WhisperOracle
     d = D.TINY_TEST
     w = weights.random_weights(d, seed=1234, emb_std=0.5)
     eng = WhisperEngine(d, device=0, max_batch=32)
@@ -141,8 +141,7 @@ def test_wide_batch_greedy_matches_fp16_oracle():
         sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
         cfg = DecodeConfig(suppress_tokens=sup, max_length=64)
         outs = eng.decode(n, cfg, dump_steps=4)
-        # 32 greedy rows take the E-form cross-attention, which never rounds K/V to fp16
-        orc = WhisperOracle(d, w, fp16=GPU_POINTS - {"xkv"} if eng.cross_attention_form(n) else True)
+        orc = WhisperOracle(d, w, fp16=True)
         for k in range(2):
             enc = eng.encoder_output(k)
             r = odec.greedy_from_encoder(orc, orc.cross_kv(enc), st,
@@ -154,40 +153,6 @@ def test_wide_batch_greedy_matches_fp16_oracle():
                 assert outs[j].tokens == outs[k].tokens
     finally:
         eng.close()
-
-
-@pytest.mark.parametrize("dims_name,n", [("TINY_TEST", 24), ("TINY_TEST", 40), ("LARGE_V3_TURBO", 24)])
-def test_eform_matches_per_head_cross_attention(monkeypatch, dims_name, n):
-    """The E-form cross-attention (greedy batches of >= 24 windows: attention over the
-    encoder output itself, V projected after the softmax) against the per-head K/V form
-    of a second context built with OSW_EFORM=0, on the same windows: the first 4
-    steps' logits within 2e-2 and identical ids.  Turbo dims (D 1280, 20 heads) take the
-    512-thread exattn_kernel instantiation, tiny dims (D 384) the 256-thread one."""
-    d = getattr(D, dims_name)
-    sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
-    cfg = DecodeConfig(suppress_tokens=sup, max_length=24 if d.n_text_state > 512 else 48)
-    pcms = [synth.chirp_clip(11 + i, 30.0 if i % 3 else 17.5) for i in range(3)]
-    w = weights.random_weights(d, seed=1234, emb_std=0.5) if d.n_text_state <= 512 else None
-    got = {}
-    for off in (False, True):
-        monkeypatch.setenv("OSW_EFORM", "0" if off else "1")
-        eng = WhisperEngine(d, device=0, max_batch=n)
-        try:
-            if w is not None:
-                eng.load_weights(w)
-            else:
-                eng.init_random(seed=5)
-            assert eng.cross_attention_form(n) == (0 if off else 1)
-            eng.log_mel([pcms[i % 3] for i in range(n)])
-            eng.encode([(i, 0, 3000) for i in range(n)])
-            got[off] = eng.decode(n, cfg, dump_steps=4)
-        finally:
-            eng.close()
-    for j in range(n):
-        for i in range(4):
-            np.testing.assert_allclose(got[False][j].logits[i], got[True][j].logits[i], atol=2e-2, rtol=0,
-                                       err_msg=f"window {j} step {i}")
-        assert got[False][j].tokens == got[True][j].tokens, j
 
 
 def test_batch_equals_single(tiny_engine):

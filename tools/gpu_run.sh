@@ -1,0 +1,61 @@
+#!/bin/bash
+# One parameterised GPU runner (replaces the per-call tools/run/r04_*.sh scripts).
+# usage: tools/gpu_run.sh TAG STEP [STEP ...]    (run through gpurun from the repo root)
+# Every step has its own time limit; the first failing step ends the call.
+#   tests       the whole -m gpu suite                      -> $O/gpu_tests.log
+#   bench       the default bench line                      -> $O/bench.json
+#   prof        one-lane kernel trace of a 3-step bench     -> $O/kernel_summary.txt (+ stats csv)
+#   pmc         FETCH_SIZE / WRITE_SIZE passes (tools/pmc_run.sh) -> $O/pmc/pmc.json
+#   stream      config-5 simulation with host breakdown     -> $O/stream.json
+#   streamprof  the same under a kernel trace, eager decode -> $O/stream_classes.txt
+#   b1          batch-1 greedy step breakdown               -> $O/b1_breakdown.txt
+#   bench:ARGS  bench.py with extra args (commas -> spaces) -> $O/bench_N.json
+#   py:SCRIPT,ARGS  python3 SCRIPT ARGS                     -> $O/py_N.txt
+cd "$GRAFT_REPO_ROOT" || exit 1
+TAG=$1; shift
+O=gpurun_out/$TAG; mkdir -p $O
+export TMPDIR=/tmp
+QUICK="--latency-repeats 0 --beam5-latency-repeats 0 --beam5 0 --beam5-steps 0 --realistic-steps 0 --stream-sessions 0 --no-cpu-baseline"
+i=0
+for s in "$@"; do
+  i=$((i+1))
+  echo "== step $i: $s ($(date +%T))"
+  case $s in
+    tests)
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -rf > $O/gpu_tests.log 2>&1
+      rc=$?; tail -5 $O/gpu_tests.log ;;
+    bench)
+      timeout -k 10 700 python -u bench.py > $O/bench.json 2> $O/bench.err; rc=$?
+      [ $rc -eq 0 ] && python3 -c "import json;d=json.load(open('$O/bench.json'));print(d['value'],d['ms_per_step'],d.get('p50_latency_ms_b1'),d.get('beam5',{}).get('value'),d.get('streaming',{}).get('transcriptions_per_s'),d['roofline']['frac'])" ;;
+    prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 3 --lanes 1 $QUICK > $O/prof.json 2> $O/prof.err
+      rc=$?; [ $rc -eq 0 ] && python3 tools/kstats.py $O/prof/run_kernel_stats.csv 30 > $O/kernel_summary.txt && head -12 $O/kernel_summary.txt
+      rm -f $O/prof/run_kernel_trace.csv ;;
+    pmc)
+      timeout -k 10 700 bash tools/pmc_run.sh $TAG/pmc; rc=$? ;;
+    stream)
+      timeout -k 10 300 python3 -u tools/stream_breakdown.py 32 6.0 $O/stream.json > $O/stream.log 2>&1; rc=$?
+      tail -40 $O/stream.log ;;
+    streamprof)
+      export OSW_NO_GRAPH=1
+      timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/sprof -o run -- python3 tools/stream_breakdown.py 32 6.0 $O/stream_prof.json > $O/stream_prof.log 2>&1
+      rc=$?; unset OSW_NO_GRAPH
+      [ $rc -eq 0 ] && python3 tools/trace_classes.py $O/sprof/run_kernel_trace.csv $O/stream_classes.txt && head -16 $O/stream_classes.txt
+      rm -f $O/sprof/run_kernel_trace.csv ;;
+    b1)
+      timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/b1prof -o run -- python3 bench.py --steps 1 --warmup 0 --lanes 1 --latency-repeats 4 --latency-warmup 1 --beam5-latency-repeats 0 --beam5 0 --beam5-steps 0 --realistic-steps 0 --stream-sessions 0 --no-cpu-baseline > $O/b1.json 2> $O/b1.err
+      rc=$?; [ $rc -eq 0 ] && python3 tools/b1_breakdown.py $O/b1prof/run_kernel_trace.csv $((5*445)) > $O/b1_breakdown.txt && head -30 $O/b1_breakdown.txt
+      rm -f $O/b1prof/run_kernel_trace.csv ;;
+    bench:*)
+      A=${s#bench:}; A=${A//,/ }
+      timeout -k 10 600 python -u bench.py $A > $O/bench_$i.json 2> $O/bench_$i.err; rc=$?
+      head -c 600 $O/bench_$i.json; echo ;;
+    py:*)
+      A=${s#py:}; A=${A//,/ }
+      timeout -k 10 600 python3 -u $A > $O/py_$i.txt 2>&1; rc=$?
+      tail -30 $O/py_$i.txt ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+  if [ $rc -ne 0 ]; then echo "step $s rc $rc: stop"; exit $rc; fi
+done
+echo "all steps done ($(date +%T))"

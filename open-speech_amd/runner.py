@@ -1,23 +1,35 @@
-"""Dynamic batcher + per-GPU workers behind ``transcribe()``.
+"""Dynamic batcher + per-GPU lanes behind ``transcribe()``.
 
 The reference calls ``transcribe`` concurrently from the default executor (REST,
 ``src/main.py:305``), a 4-thread streaming pool (``src/streaming.py:50-52``), a
 4-thread Realtime pool (``src/realtime/server.py:33-35``) and Wyoming.  Each call
-here becomes a request on a queue; one worker thread per GPU drains up to
-``max_batch`` requests (waiting at most ``max_wait_ms`` for company once the first
-arrives, and at most ``gap_ms`` after the latest arrival), runs them as one batched seek loop on its engine, and completes each
-caller's future.  Requests are routed to the worker with the shortest queue
-(multi-GPU serving: independent clips, no collective).  A worker whose GPU fails
-marks every worker of that GPU (its sibling lanes) dead and re-queues the requests
-it held that are still unanswered on the workers of the other GPUs.
+here becomes a request on its GPU's queue (requests go to the GPU with the fewest
+queued + running requests; multi-GPU serving shards independent clips, no
+collective).  The lanes of a GPU (contexts sharing one weight copy, one host thread
+each) pull batches from that queue: a free lane that finds the queue non-empty waits
+for company (at most ``max_wait_ms`` after the oldest request, ``gap_ms`` after the
+latest), takes up to ``max_batch`` requests and runs them as one batched seek loop.
+
+Pipelining (``split``): when no other lane of the GPU is running a batch, the lane
+takes only half of what is queued (rounded up) and leaves the rest to the next free
+lane, which takes it at once.  The sibling lanes' encoders are serialised on the GPU
+(the encoder baton, ``osw_set_encoder_baton_min``), so the second batch encodes while
+the first decodes.  Under the streaming pool's closed loop (4 calls in flight, each
+session waiting for its call) this turns lock-step batches of 4 — encode 4, decode
+4, nothing overlapping — into two staggered batches of 2 whose encoder and decoder
+phases overlap.  With a deep queue (REST load) both halves are ``max_batch`` anyway.
+
+A lane whose GPU fails marks every lane of that GPU dead, moves the GPU's queued
+requests to the other GPUs and re-queues there the requests of its batch that are
+still unanswered.
 """
 from __future__ import annotations
 
-import queue
 import threading
 import time
+from collections import deque
 from concurrent.futures import Future
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import numpy as np
 
@@ -30,46 +42,89 @@ class _Req:
     pcm: np.ndarray
     opts: TranscribeOptions
     fut: Future
+    t_enq: float = field(default=0.0)
+
+
+class _DevQueue:
+    """The request queue of one GPU, shared by its lanes."""
+
+    def __init__(self, device):
+        self.device = device
+        self.items: deque = deque()
+        self.cv = threading.Condition()
+        self.lanes: list = []
+        self.collecting = False     # a lane is waiting for company for its batch
+        self.alive = True
+        self.closing = False
+
+    def load(self) -> int:
+        return len(self.items) + sum(w.inflight for w in self.lanes)
+
+    def put(self, r: _Req) -> None:
+        with self.cv:
+            r.t_enq = time.monotonic()
+            self.items.append(r)
+            self.cv.notify_all()
 
 
 class _Worker(threading.Thread):
-    def __init__(self, pool: "BatchRunner", engine, idx: int):
-        super().__init__(daemon=True, name=f"osw-worker-{idx}")
-        self.pool, self.engine, self.idx = pool, engine, idx
-        self.q: "queue.Queue[_Req | None]" = queue.Queue()
+    def __init__(self, pool: "BatchRunner", engine, idx: int, dq: _DevQueue):
+        super().__init__(daemon=True, name=f"osw-lane-{idx}")
+        self.pool, self.engine, self.idx, self.dq = pool, engine, idx, dq
         self.alive = True
         self.inflight = 0
 
-    def load(self) -> int:
-        return self.q.qsize() + self.inflight
+    @property
+    def q(self) -> _DevQueue:
+        return self.dq
+
+    def _take(self) -> list | None:
+        """Block until a batch is ready for this lane; None when the runner closes."""
+        dq, pool = self.dq, self.pool
+        with dq.cv:
+            while True:
+                if dq.closing or not self.alive:
+                    return None
+                if dq.items and not dq.collecting:
+                    break
+                dq.cv.wait()
+            dq.collecting = True
+            try:
+                gap = pool.gap_ms / 1000.0 if pool.gap_ms is not None else None
+                cap = self.engine.max_batch
+                while len(dq.items) < cap and not dq.closing and self.alive:
+                    # wait for company until max_wait after the oldest request, or gap after the
+                    # latest one (callers released together by the previous batch arrive within
+                    # a fraction of a millisecond; waiting the whole max_wait for a 5th that the
+                    # 4-thread streaming pool can never send cost ~4 ms per call)
+                    end = dq.items[0].t_enq + pool.max_wait_ms / 1000.0
+                    if gap is not None:
+                        end = min(end, dq.items[-1].t_enq + gap)
+                    left = end - time.monotonic()
+                    if left <= 0:
+                        break
+                    dq.cv.wait(timeout=left)
+                if dq.closing or not self.alive or not dq.items:
+                    return None if (dq.closing or not self.alive) else []
+                k = min(cap, len(dq.items))
+                others_busy = any(w.inflight for w in dq.lanes if w is not self)
+                idle_sibling = any(w.alive and not w.inflight for w in dq.lanes if w is not self)
+                if pool.split and not others_busy and idle_sibling:
+                    k = min(k, (len(dq.items) + 1) // 2)
+                batch = [dq.items.popleft() for _ in range(k)]
+                self.inflight = len(batch)
+                return batch
+            finally:
+                dq.collecting = False
+                dq.cv.notify_all()
 
     def run(self) -> None:
         while True:
-            first = self.q.get()
-            if first is None:
+            batch = self._take()
+            if batch is None:
                 return
-            batch = [first]
-            now = time.monotonic()
-            deadline = now + self.pool.max_wait_ms / 1000.0
-            gap = self.pool.gap_ms / 1000.0 if self.pool.gap_ms is not None else None
-            last = now
-            while len(batch) < self.engine.max_batch:
-                # wait for company until max_wait after the first request, or gap after the
-                # latest one (callers released together by the previous batch arrive within
-                # a fraction of a millisecond; waiting the whole max_wait for a 5th that the
-                # 4-thread streaming pool can never send cost ~4 ms per call)
-                end = deadline if gap is None else min(deadline, last + gap)
-                left = end - time.monotonic()
-                try:
-                    nxt = self.q.get(timeout=max(0.0, left)) if left > 0 else self.q.get_nowait()
-                except queue.Empty:
-                    break
-                if nxt is None:
-                    self.q.put(None)
-                    break
-                batch.append(nxt)
-                last = time.monotonic()
-            self.inflight = len(batch)
+            if not batch:
+                continue
             try:
                 self._run_batch(batch)
             except Exception as e:  # noqa: BLE001 - forwarded to callers
@@ -78,12 +133,15 @@ class _Worker(threading.Thread):
                     for r in batch:
                         if not r.fut.done():
                             self.pool.submit_req(r)
+                    self.inflight = 0
                     return
                 for r in batch:
                     if not r.fut.done():
                         r.fut.set_exception(e)
             finally:
-                self.inflight = 0
+                with self.dq.cv:
+                    self.inflight = 0
+                    self.dq.cv.notify_all()
 
     def _run_batch(self, batch: list) -> None:
         groups: dict = {}
@@ -99,13 +157,26 @@ class _Worker(threading.Thread):
 
 class BatchRunner:
     def __init__(self, engines: list, tokenizer: WhisperTokenizer, max_wait_ms: float = 5.0,
-                 gap_ms: float | None = None):
+                 gap_ms: float | None = None, split: bool = True):
         self.tokenizer = tokenizer
         self.max_wait_ms = max_wait_ms
         self.gap_ms = gap_ms
+        self.split = split
         self._sup_cache: dict = {}
         self._lock = threading.Lock()
-        self.workers = [_Worker(self, e, i) for i, e in enumerate(engines)]
+        self.queues: list[_DevQueue] = []
+        by_dev: dict = {}
+        self.workers = []
+        for i, e in enumerate(engines):
+            dev = getattr(e, "device", None)
+            key = ("dev", dev) if dev is not None else ("engine", i)
+            if key not in by_dev:
+                by_dev[key] = _DevQueue(dev)
+                self.queues.append(by_dev[key])
+            dq = by_dev[key]
+            w = _Worker(self, e, i, dq)
+            dq.lanes.append(w)
+            self.workers.append(w)
         for w in self.workers:
             w.start()
 
@@ -123,45 +194,35 @@ class BatchRunner:
         s = str(e)
         return "hipError" in s or "(-100)" in s
 
-    @staticmethod
-    def _device_of(w: _Worker):
-        return getattr(w.engine, "device", None)
-
     def fail_device(self, failed: _Worker) -> bool:
-        """Mark every worker on `failed`'s GPU dead (lanes share the device) and move their
-        queued requests to the survivors.  False when no other GPU's worker is alive
-        (the error then goes to the callers)."""
-        dev = self._device_of(failed)
-        same = [w for w in self.workers if w is failed or (dev is not None and self._device_of(w) == dev)]
+        """Mark every lane of `failed`'s GPU dead (lanes share the device) and move that
+        GPU's queued requests to the survivors.  False when no other GPU is alive (the
+        error then goes to the callers)."""
+        dq = failed.dq
         with self._lock:
-            if not any(w.alive and w not in same for w in self.workers):
+            if not any(q.alive for q in self.queues if q is not dq):
                 return False
-            for w in same:
+            dq.alive = False
+        with dq.cv:
+            for w in dq.lanes:
                 w.alive = False
-        for w in same:
-            self.drain_dead(w)
-            if w is not failed:
-                w.q.put(None)   # its thread exits after the batch it may be running
+            moved = list(dq.items)
+            dq.items.clear()
+            dq.cv.notify_all()
+        for r in moved:
+            if not r.fut.done():
+                self.submit_req(r)
         return True
 
-    def submit_req(self, r: _Req, exclude=None) -> None:
+    def submit_req(self, r: _Req) -> None:
         with self._lock:
-            live = [w for w in self.workers if w.alive and w is not exclude]
+            live = [q for q in self.queues if q.alive]
             if not live:
                 if not r.fut.done():
                     r.fut.set_exception(RuntimeError("no live GPU worker"))
                 return
-            w = min(live, key=lambda x: x.load())
-            w.q.put(r)
-
-    def drain_dead(self, dead: _Worker) -> None:
-        while True:
-            try:
-                r = dead.q.get_nowait()
-            except queue.Empty:
-                return
-            if r is not None and not r.fut.done():
-                self.submit_req(r, exclude=dead)
+            q = min(live, key=lambda x: x.load())
+        q.put(r)
 
     def submit(self, pcm: np.ndarray, opts: TranscribeOptions) -> Future:
         f: Future = Future()
@@ -172,11 +233,17 @@ class BatchRunner:
         return self.submit(pcm, opts).result(timeout=timeout)
 
     def close(self) -> None:
-        for w in self.workers:
-            if w.is_alive():
-                w.q.put(None)
+        for q in self.queues:
+            with q.cv:
+                q.closing = True
+                q.cv.notify_all()
         for w in self.workers:
             w.join(timeout=30)
+        for q in self.queues:
+            for r in q.items:
+                if not r.fut.done():
+                    r.fut.set_exception(RuntimeError("runner closed"))
+            q.items.clear()
         for w in self.workers:
             close = getattr(w.engine, "close", None)
             if close:

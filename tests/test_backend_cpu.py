@@ -308,7 +308,9 @@ def test_non_wav_rejected_or_converted():
 def test_device_error_fails_over_to_other_gpu():
     """A HIP error in the second opts-group of a batch: the first group's answers stand,
     only the unanswered requests move, and they skip the failed GPU's sibling lane
-    (runner.py re-queued answered requests onto a lane of the same GPU)."""
+    (runner.py re-queued answered requests onto a lane of the same GPU).
+    Both lanes of GPU 0 fail on their second decode; whichever takes the batch fails,
+    and the other never decodes."""
     from open_speech_amd._lib import OswDeviceError
     from open_speech_amd.runner import BatchRunner
     from open_speech_amd.segments import TranscribeOptions
@@ -326,8 +328,8 @@ def test_device_error_fails_over_to_other_gpu():
                 raise OswDeviceError("osw_decode_windows failed (-100): hipErrorLaunchFailure", -100)
             return super().decode(n, cfg, prefix, dump_steps, languages)
 
-    a, a2, b = Eng(0, 1, fail_on_call=2), Eng(0, 2), Eng(1, 3)
-    runner = BatchRunner([a, a2, b], WhisperTokenizer(51866), max_wait_ms=300)
+    a, a2, b = Eng(0, 1, fail_on_call=2), Eng(0, 1, fail_on_call=2), Eng(1, 3)
+    runner = BatchRunner([a, a2, b], WhisperTokenizer(51866), max_wait_ms=300, split=False)
     try:
         from concurrent.futures import Future
         from open_speech_amd.runner import _Req
@@ -336,12 +338,12 @@ def test_device_error_fails_over_to_other_gpu():
             opts = TranscribeOptions(beam_size=1, language="en" if i < 2 else "de")
             reqs.append(_Req(synth.chirp_clip(i, 4.0), opts, Future()))
         for r in reqs:
-            runner.workers[0].q.put(r)
+            runner.workers[0].q.put(r)   # GPU 0's queue
         res = [r.fut.result(timeout=30) for r in reqs]
         assert [sg.tokens for sg in res[0].segments] == [[TB, 1001, TB + 50]]   # group 1 answered by GPU 0
         assert all(sg.tokens == [TB, 1003, TB + 50] for r in res[2:] for sg in r.segments)  # moved to GPU 1
         assert not runner.workers[0].alive and not runner.workers[1].alive and runner.workers[2].alive
-        assert a2.n_decode == 0
+        assert a.n_decode + a2.n_decode == 2   # one batch: group 1 answered, group 2 failed
         # new work avoids the failed GPU
         assert [sg.tokens for sg in runner.transcribe(synth.chirp_clip(9, 3.0), TranscribeOptions(beam_size=1,
                 language="en")).segments] == [[TB, 1003, TB + 50]]
@@ -401,5 +403,40 @@ def test_batcher_gap_ends_collection_early():
             r.fut.result(timeout=30)
         assert e.batches and set(e.batches) == {3}   # every seek-loop call carries all three
         assert _t.monotonic() - t0 < 1.5   # not the 2 s max_wait
+    finally:
+        runner.close()
+
+
+@pytest.mark.parametrize("split,want", [(True, [2, 2]), (False, [4])])
+def test_split_pipelines_lanes(split, want):
+    """Pipelined lanes (runner.py): 4 requests queued together on a GPU with 3 idle lanes
+    go out as two batches of 2 (the first lane takes half, the next free lane the rest at
+    once), so one batch can encode while the other decodes; without split, one batch."""
+    from concurrent.futures import Future
+    from open_speech_amd.runner import BatchRunner, _Req
+    from open_speech_amd.segments import TranscribeOptions
+    from open_speech_amd.tokenizer import WhisperTokenizer
+
+    class Eng(FakeEngine):
+        def __init__(self):
+            super().__init__(D.MICRO_TEST, 0, 8,
+                             lambda w, i, p, l: WindowOutput([TB, 1000, TB + 50], -1.0, 0.01, ST.first_lang))
+            self.device = 0
+
+        def decode(self, n, cfg, prefix=None, dump_steps=0, languages=None):
+            time.sleep(0.05)
+            return super().decode(n, cfg, prefix, dump_steps, languages)
+
+    es = [Eng(), Eng(), Eng()]
+    runner = BatchRunner(es, WhisperTokenizer(51866), max_wait_ms=500, gap_ms=30, split=split)
+    try:
+        assert len(runner.queues) == 1
+        reqs = [_Req(synth.chirp_clip(i, 3.0), TranscribeOptions(beam_size=1, language="en"), Future())
+                for i in range(4)]
+        for r in reqs:
+            runner.submit_req(r)
+        for r in reqs:
+            assert r.fut.result(timeout=30).segments
+        assert sorted(b for e in es for b in e.batches) == want
     finally:
         runner.close()

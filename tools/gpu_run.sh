@@ -11,6 +11,8 @@
 #   b1          batch-1 greedy step breakdown               -> $O/b1_breakdown.txt
 #   bench:ARGS  bench.py with extra args (commas -> spaces) -> $O/bench_N.json
 #   py:SCRIPT,ARGS  python3 SCRIPT ARGS                     -> $O/py_N.txt
+#   env:A=1,B=2 / unenv:A,B   set / clear environment variables for the following steps
+# stream and streamprof write $O/stream[_prof]_N.json when run more than once (N = step index)
 cd "$GRAFT_REPO_ROOT" || exit 1
 TAG=$1; shift
 O=gpurun_out/$TAG; mkdir -p $O
@@ -34,14 +36,18 @@ for s in "$@"; do
     pmc)
       timeout -k 10 700 bash tools/pmc_run.sh $TAG/pmc; rc=$? ;;
     stream)
-      timeout -k 10 300 python3 -u tools/stream_breakdown.py 32 6.0 $O/stream.json > $O/stream.log 2>&1; rc=$?
-      tail -40 $O/stream.log ;;
+      timeout -k 10 300 python3 -u tools/stream_breakdown.py 32 6.0 $O/stream_$i.json > $O/stream_$i.log 2>&1; rc=$?
+      python3 -c "import json;d=json.load(open('$O/stream_$i.json'));s=d['sim'];print('calls/s',s['transcriptions_per_s'],'lag p50',s['final_transcript_lag_p50_s'],'batches',d['batch_size_hist'],'conc',d['concurrent_lanes_s'])" ;;
+    env:*)
+      A=${s#env:}; for kv in ${A//,/ }; do export "$kv"; echo "export $kv"; done; rc=0 ;;
+    unenv:*)
+      A=${s#unenv:}; for k in ${A//,/ }; do unset "$k"; done; rc=0 ;;
     streamprof)
       export OSW_NO_GRAPH=1
-      timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/sprof -o run -- python3 tools/stream_breakdown.py 32 6.0 $O/stream_prof.json > $O/stream_prof.log 2>&1
+      timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/sprof_$i -o run -- python3 tools/stream_breakdown.py 32 6.0 $O/stream_prof_$i.json > $O/stream_prof_$i.log 2>&1
       rc=$?; unset OSW_NO_GRAPH
-      [ $rc -eq 0 ] && python3 tools/trace_classes.py $O/sprof/run_kernel_trace.csv $O/stream_classes.txt && head -16 $O/stream_classes.txt
-      rm -f $O/sprof/run_kernel_trace.csv ;;
+      [ $rc -eq 0 ] && python3 tools/trace_classes.py $O/sprof_$i/run_kernel_trace.csv $O/stream_classes_$i.txt && head -16 $O/stream_classes_$i.txt
+      rm -f $O/sprof_$i/run_kernel_trace.csv ;;
     b1)
       timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/b1prof -o run -- python3 bench.py --steps 1 --warmup 0 --lanes 1 --latency-repeats 4 --latency-warmup 1 --beam5-latency-repeats 0 --beam5 0 --beam5-steps 0 --realistic-steps 0 --stream-sessions 0 --no-cpu-baseline > $O/b1.json 2> $O/b1.err
       rc=$?; [ $rc -eq 0 ] && python3 tools/b1_breakdown.py $O/b1prof/run_kernel_trace.csv $((5*445)) > $O/b1_breakdown.txt && head -30 $O/b1_breakdown.txt

@@ -47,8 +47,12 @@ class TensorSpec:
         return n
 
 
-def canonical_specs(d: WhisperDims, *, w_std: float = 0.02, emb_std: float = 0.02) -> list[TensorSpec]:
-    """All tensors of the model, in a fixed order (the index is the hash stream id)."""
+def canonical_specs(d: WhisperDims, *, w_std: float = 0.02, emb_std: float = 0.02,
+                    pos_std: float = 0.02, out_gain: float = 1.0) -> list[TensorSpec]:
+    """All tensors of the model, in a fixed order (the index is the hash stream id).
+    ``pos_std`` / ``out_gain``: the decoder's positional-embedding scale and the final
+    LayerNorm's gain (the goldens raise both so that greedy decoding of random weights
+    emits varied text with clear top-2 margins; tools/make_golden.py)."""
     De, Dd, M = d.n_audio_state, d.n_text_state, d.n_mels
     u = math.sqrt(3.0)  # uniform[-a, a) has std a/sqrt(3)
     W = w_std * u
@@ -86,7 +90,7 @@ def canonical_specs(d: WhisperDims, *, w_std: float = 0.02, emb_std: float = 0.0
     ln("enc.lnpost", De)
 
     mat("dec.tok", (d.n_vocab, Dd), emb_std * u)
-    vec("dec.pos", d.n_text_ctx * Dd, 0.02 * u)
+    vec("dec.pos", d.n_text_ctx * Dd, pos_std * u)
     L = d.n_text_layer
     mat("dec.crosskv.w", (L * 2 * Dd, De))
     # per layer: [k bias (zero) | v bias]
@@ -108,7 +112,8 @@ def canonical_specs(d: WhisperDims, *, w_std: float = 0.02, emb_std: float = 0.0
         vec(p + ".fc1.b", 4 * Dd)
         mat(p + ".fc2.w", (Dd, 4 * Dd))
         vec(p + ".fc2.b", Dd)
-    ln("dec.lnpost", Dd)
+    vec("dec.lnpost.g", Dd, G * out_gain, out_gain)
+    vec("dec.lnpost.b", Dd, B)
     return s
 
 
@@ -155,6 +160,56 @@ def hash_uniform(seed: int, stream: int, n: int, scale: float, offset: float) ->
     return out
 
 
+def hash_uniform_at(seed: int, stream: int, idx: np.ndarray, scale: float, offset: float) -> np.ndarray:
+    """The elements ``idx`` of ``hash_uniform(seed, stream, ...)`` (same values)."""
+    key = np.uint64(stream_key(seed, stream))
+    with np.errstate(over="ignore"):
+        h = _splitmix64(np.asarray(idx, dtype=np.uint64) + key)
+    u = (h >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    return (u * np.float32(2.0) - np.float32(1.0)) * np.float32(scale) + np.float32(offset)
+
+
+TEXT_TS_AMP = 0.6     # weight of the timestamp target relative to the text target
+
+
+def text_targets(d: WhisperDims, seed: int) -> tuple[np.ndarray, np.ndarray]:
+    """The two target tokens of every decoder position (``text_positional``): a
+    pseudo-random text token below <|endoftext|>, and a timestamp token that rises
+    with the position (first ones <= 1.00 s, as the initial-timestamp rule requires)."""
+    from .dims import SpecialTokens
+    st = SpecialTokens.for_vocab(d.n_vocab)
+    n = d.n_text_ctx
+    v = hash_uniform(seed, 9002, n, 0.5, 0.5).astype(np.float64)
+    text = np.minimum((v * st.eot).astype(np.int64), st.eot - 1)
+    ts = st.timestamp_begin + np.minimum((np.arange(n) * 1400) // n, 1500)
+    return text, ts
+
+
+def text_positional(d: WhisperDims, seed: int, amp: float, noise: float = 1.0, **spec_kw) -> np.ndarray:
+    """A decoder positional table that makes greedy decoding of random weights emit
+    varied text with clear top-2 margins (the "text" goldens, tools/make_golden.py):
+    pos[p] = amp * (tok[text(p)] + TEXT_TS_AMP * tok[ts(p)]) + uniform noise of std
+    ``noise``, where tok is the (fp16) token-embedding table of
+    ``random_weights(d, seed, **spec_kw)`` and text(p) / ts(p) the position's targets
+    (``text_targets``).  With the tied output projection the hidden state at position
+    p leans towards text(p), and towards ts(p) where the timestamp rules force a
+    timestamp, so ids change every step and rule-forced steps are not near-ties (the
+    i.i.d. default init decodes near-ties between thousands of tokens, or timestamp
+    pairs and a handful of repeated tokens).  The rest of the model is unchanged."""
+    specs = canonical_specs(d, **spec_kw)
+    i_tok = next(i for i, sp in enumerate(specs) if sp.name == "dec.tok")
+    D = d.n_text_state
+    text, ts = text_targets(d, seed)
+
+    def rows(t):
+        idx = (t[:, None] * D + np.arange(D)[None, :]).reshape(-1)
+        return hash_uniform_at(seed, i_tok, idx, specs[i_tok].scale, 0.0).astype(np.float16).astype(np.float32)
+
+    nz = hash_uniform(seed, 9003, d.n_text_ctx * D, noise * math.sqrt(3.0), 0.0)
+    x = np.float32(amp) * (rows(text) + np.float32(TEXT_TS_AMP) * rows(ts)) + nz
+    return x.reshape(d.n_text_ctx, D).astype(np.float32)
+
+
 def sinusoids(length: int, channels: int, max_timescale: float = 10000.0) -> np.ndarray:
     """Encoder positional table (openai-whisper ``sinusoids``; transformers
     modeling_whisper.py:55).  Real checkpoints store this table; random init regenerates it."""
@@ -180,8 +235,13 @@ def make_tensor(spec: TensorSpec, d: WhisperDims, seed: int, stream: int) -> np.
     return x.astype(np.float16) if spec.dtype == F16 else x
 
 
-def random_weights(d: WhisperDims, seed: int = 0, **kw) -> dict[str, np.ndarray]:
-    return {sp.name: make_tensor(sp, d, seed, i) for i, sp in enumerate(canonical_specs(d, **kw))}
+def random_weights(d: WhisperDims, seed: int = 0, text_pos: float | None = None, **kw) -> dict[str, np.ndarray]:
+    """The canonical hash-initialised weights; ``text_pos`` (an amplitude): the decoder
+    positional table of ``text_positional`` instead of the i.i.d. one."""
+    w = {sp.name: make_tensor(sp, d, seed, i) for i, sp in enumerate(canonical_specs(d, **kw))}
+    if text_pos:
+        w["dec.pos"] = text_positional(d, seed, text_pos, **kw)
+    return w
 
 
 # --------------------------------------------------------------------------

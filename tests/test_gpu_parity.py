@@ -122,6 +122,29 @@ def test_tiny_greedy_matches_fp16_oracle(tiny_engine):
     assert out.language == r.language
 
 
+def test_tiny_text_greedy_matches_golden():
+    """The varied-text tiny golden (tools/make_golden.py gen_tiny_text): every one of
+    the 445 greedy ids identical on the GPU (golden min top-2 margin in meta.json)."""
+    import json
+    m = json.load(open(os.path.join(GOLD, "meta.json")))["tiny_text"]
+    z = np.load(os.path.join(GOLD, "tiny_text.npz"))
+    d = D.TINY_TEST
+    eng = WhisperEngine(d, device=0, max_batch=2)
+    try:
+        eng.load_weights(weights.random_weights(d, seed=m["seed"], text_pos=m["text_pos"]))
+        eng.log_mel([synth.chirp_clip(3, 30.0)])
+        eng.encode([(0, 0, 3000)])
+        sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+        out = eng.decode(1, DecodeConfig(suppress_tokens=sup))[0]
+        want = z["ids"].tolist()
+        assert len(set(want)) >= 150
+        assert out.language == int(z["language"])
+        assert out.tokens == want, next(k for k in range(min(len(want), len(out.tokens)))
+                                        if k >= len(out.tokens) or out.tokens[k] != want[k])
+    finally:
+        eng.close()
+
+
 def test_wide_batch_greedy_matches_fp16_oracle():
     """>= 24 decoder rows take the 3-slot ring logits GEMM (gemm_wide_kernel) instead of
     the skinny one: 32 windows (two clips alternating) against the fp16 oracle, and every

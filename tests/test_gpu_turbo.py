@@ -15,6 +15,12 @@ Beam search width 5 (the reference's decoding, src/backends/faster_whisper.py:23
 is checked against tests/golden/turbo_beam5.npz: the oracle's CTranslate2-BeamSearch
 restatement driven by the fp32 transformers decoder on the same weights and clip
 (tools/make_golden.py gen_turbo_beam), 93 sampled positions.
+
+The i.i.d. weights above decode few distinct ids (timestamp pairs, repeated tokens), so
+their id checks barely discriminate.  The "text" goldens (tests/golden/turbo_text.npz,
+weights.text_positional) decode ~440 distinct ids in 445 steps on each of three clips
+with a golden top-2 margin >= 0.04 at every step; their ids are checked exactly, with the
+same 1e-3 log-softmax bar, and beam 5 on them.
 """
 import os
 
@@ -151,3 +157,104 @@ def test_turbo_beam5_batch64_equals_single_windows(turbo):
         assert abs(one.sum_logprob - batch[i].sum_logprob) <= 1e-4 * (len(one.tokens) + 1) + \
             1e-4 * abs(one.sum_logprob), i
     assert batch[0].tokens == z["ids"].tolist()
+
+
+# --------------------------------------------------------------------------- text goldens
+# tests/golden/turbo_text.npz (tools/make_golden.py gen_turbo_text): the same model with the
+# "text" positional table (weights.text_positional), so greedy decoding emits varied text:
+# ~440 distinct ids in 445 steps per clip, golden top-2 margin >= 0.04 at every step (meta.json
+# "turbo_text"), three clips.  Free-running ids must be identical over all 445 steps; a
+# decoder that copies its previous token, or drops a layer, cannot pass.
+TEXT = os.path.join(GOLD, "turbo_text.npz")
+
+
+def _meta(key):
+    import json
+    return json.load(open(os.path.join(GOLD, "meta.json")))[key]
+
+
+@pytest.fixture(scope="module")
+def turbo_text():
+    d = D.LARGE_V3_TURBO
+    m = _meta("turbo_text")
+    eng = WhisperEngine(d, device=0, max_batch=8)
+    eng.init_random(seed=m["seed"], text_pos=m["text_pos"])
+    sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+    yield d, eng, sup, np.load(TEXT), m
+    eng.close()
+
+
+def _text_clip(name):
+    return {"chirp0": lambda: synth.chirp_clip(0, 30.0), "tone": lambda: synth.tone_clip(30.0),
+            "chirp1": lambda: synth.chirp_clip(1, 30.0)}[name]()
+
+
+def _lsm_err(out_logits, z, pre, n_steps):
+    full_at = {int(t): i for i, t in enumerate(z[pre + "full_steps"])}
+    errs, n_full = [], 0
+    for s in range(n_steps):
+        g = out_logits[s].astype(np.float64)
+        lg = lse(g)
+        if s in full_at:
+            ref = z[pre + "full_logits"][full_at[s]].astype(np.float64) - z[pre + "lse"][s]
+            errs.append(np.abs((g - lg) - ref).max())
+            n_full += 1
+        ids = z[pre + "sub_ids"][s]
+        errs.append(np.abs((g[ids] - lg) - (z[pre + "sub_vals"][s].astype(np.float64) - z[pre + "lse"][s])).max())
+    return max(errs), n_full
+
+
+@pytest.mark.parametrize("clip", ["chirp0", "tone", "chirp1"])
+def test_turbo_text_greedy_ids_exact(turbo_text, clip):
+    """Varied-text golden, one window: every one of the 445 greedy ids identical, language
+    and no-speech prob equal, and the log-softmax of the raw logits within 1e-3 (over the
+    whole vocabulary at the first 4 steps, and every 32nd for chirp0; over 288 tokens per
+    step at every step)."""
+    d, eng, sup, z, m = turbo_text
+    pre = clip + "/"
+    eng.log_mel([_text_clip(clip)])
+    eng.encode([(0, 0, 3000)])
+    enc = eng.encoder_output(0)
+    np.testing.assert_allclose(np.linalg.norm(enc.astype(np.float64), axis=1), z[pre + "enc_rownorm"], rtol=1e-3)
+    want = z[pre + "ids"].tolist()
+    assert len(set(want)) >= 150 and len(want) >= 300   # the golden itself is discriminative
+    out = eng.decode(1, DecodeConfig(suppress_tokens=sup), dump_steps=len(want) + 1)[0]
+    assert out.language == int(z[pre + "language"])
+    assert abs(out.no_speech_prob - float(z[pre + "no_speech_prob"])) < 1e-3
+    k = first_divergence(out.tokens, want, None)
+    n_ok = len(want) + 1 if k is None else k + 1
+    err, n_full = _lsm_err(out.logits, z, pre, min(n_ok, len(z[pre + "lse"])))
+    print(f"turbo text {clip}: {len(out.tokens)} ids ({len(set(out.tokens))} distinct), divergence at {k}, "
+          f"log-softmax max |d| {err:.3e} ({n_full} full-vocabulary steps), golden min margin "
+          f"{float(z[pre + 'margins'].min()):.3g}")
+    assert k is None, (f"ids diverge at step {k}: gpu {out.tokens[k:k + 4]} vs golden {want[k:k + 4]}, golden "
+                       f"top-2 margin {float(z[pre + 'margins'][k]):.4g}")
+    assert err <= LSM_TOL, err
+    assert abs(out.sum_logprob - float(z[pre + "sum_logprob"])) <= 1e-4 * (len(want) + 1)
+
+
+def test_turbo_text_batch_equals_golden(turbo_text):
+    """The three clips in one batch (3 decoder rows): every window's ids equal the golden."""
+    d, eng, sup, z, m = turbo_text
+    names = ["chirp0", "tone", "chirp1"]
+    outs = eng.transcribe_batch([_text_clip(n) for n in names], DecodeConfig(suppress_tokens=sup))
+    for n, o in zip(names, outs):
+        assert o.tokens == z[n + "/ids"].tolist(), n
+
+
+def test_turbo_text_beam5_matches_golden(turbo_text):
+    """Beam 5 (the reference's decoding) on the varied-text weights: ids identical to the
+    oracle's CTranslate2-BeamSearch restatement over the fp32 transformers decoder,
+    cumulative log-prob within 1e-4 per token."""
+    d, eng, sup, z, m = turbo_text
+    eng.log_mel([_text_clip("chirp0")])
+    eng.encode([(0, 0, 3000)])
+    cfg = DecodeConfig(suppress_tokens=sup, max_length=int(z["beam5/max_length"]), beam_size=5)
+    out = eng.decode(1, cfg)[0]
+    want = z["beam5/ids"].tolist()
+    assert len(set(want)) >= 60
+    assert out.language == int(z["beam5/language"])
+    k = first_divergence(out.tokens, want, None)
+    assert k is None, f"beam ids diverge at step {k}: gpu {out.tokens[k:k + 4]} vs golden {want[k:k + 4]}"
+    ref = float(z["beam5/sum_logprob"])
+    assert abs(out.sum_logprob - ref) <= 1e-4 * (len(want) + 1) + 1e-3 * abs(ref), (out.sum_logprob, ref)

@@ -89,6 +89,29 @@ def test_tiny_greedy_fp32_matches_transformers(tiny):
     assert abs(r.sum_logprob - float(z["sum_logprob"])) < 1e-2 * max(1.0, abs(float(z["sum_logprob"])))
 
 
+def test_tiny_text_greedy_fp32_matches_transformers():
+    """The varied-text tiny golden (weights.text_positional; ~440 distinct ids in 445
+    steps, min top-2 margin in meta.json): the oracle's fp32 greedy decode reproduces
+    every id, the language and the no-speech prob."""
+    import json
+    m = json.load(open(os.path.join(GOLD, "meta.json")))["tiny_text"]
+    z = np.load(os.path.join(GOLD, "tiny_text.npz"))
+    d = D.TINY_TEST
+    w = weights.random_weights(d, seed=m["seed"], text_pos=m["text_pos"])
+    st = D.SpecialTokens.for_vocab(d.n_vocab)
+    orc = WhisperOracle(d, w, fp16=False)
+    sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+    r = odec.greedy_from_encoder(orc, orc.cross_kv(orc.encode(z["mel"])), st,
+                                 opts=odec.DecodeOptions(suppress_tokens=sup), keep_logits=8)
+    want = z["ids"].tolist()
+    assert len(set(want)) >= 150 and len(want) >= 300
+    assert r.language == int(z["language"])
+    assert abs(r.no_speech_prob - float(z["no_speech_prob"])) < 1e-4
+    for i in range(8):
+        np.testing.assert_allclose(r.step_logits[i], z["full_logits"][i], atol=2e-3, rtol=0)
+    assert r.tokens == want
+
+
 @pytest.mark.slow
 def test_turbo_encoder_layer_fp32_matches_transformers():
     z = np.load(os.path.join(GOLD, "turbo_enc_layer0.npz"))

@@ -332,6 +332,146 @@ def gen_turbo_beam(out):
             "n_ids": len(r.tokens), "language": int(r.language)}
 
 
+# "text" goldens: weights whose greedy decoding emits varied text (weights.text_positional:
+# the decoder positional table leans every position towards a pseudo-random target token),
+# so an id check discriminates (the i.i.d. init above decodes timestamp pairs and a handful
+# of repeated tokens: 10 distinct ids in 445).  The rest of the model is the default init.
+TEXT_SEED = 11
+TEXT_AMP = 20.0         # turbo: min top-2 margin 0.04 over 3 x 445 steps, ~440 distinct ids per clip
+TINY_TEXT_AMP = 200.0   # tiny dims: the GPU's tiny encoder is held to 1e-2, so larger margins (min 1.4)
+TEXT_CLIPS = {"chirp0": lambda: synth.chirp_clip(0, 30.0), "tone": lambda: synth.tone_clip(30.0),
+              "chirp1": lambda: synth.chirp_clip(1, 30.0)}
+
+
+def greedy_golden(model, d, enc, full_every: int | None, n_full_first: int = 4):
+    """Greedy decoding of one window to <|endoftext|> or n_text_ctx positions with the
+    openai / faster-whisper logits rules, on the fp32 transformers model: ids, the
+    chosen log-probs, top-2 margins (after the rules), per-step lse and the logits of
+    the step's top-32 + a fixed 256-token sample, and the full raw logits at the first
+    n_full_first steps and every full_every-th step (None: first steps only)."""
+    st = D.SpecialTokens.for_vocab(d.n_vocab)
+    suppress = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+    gc = GenerationConfig(no_timestamps_token_id=st.no_timestamps, eos_token_id=st.eot,
+                          max_initial_timestamp_index=50)
+
+    def step(ids, past):
+        with torch.no_grad():
+            o = model(encoder_outputs=(enc,), decoder_input_ids=torch.tensor([ids]), past_key_values=past,
+                      use_cache=True)
+        return o.logits[0, -1].double(), o.past_key_values
+
+    lg, past = step([st.sot], None)
+    sot_logits = lg.float().numpy().copy()
+    lang = st.first_lang + int(np.argmax(sot_logits[st.first_lang:st.first_lang + st.n_langs]))
+    nsp = float(torch.softmax(lg, -1)[st.no_speech])
+    prompt = [st.sot, lang, st.transcribe]
+    lg, past = step([lang], past)
+    lg, past = step([st.transcribe], past)
+    begin = len(prompt)
+    procs = [SuppressTokensAtBeginLogitsProcessor([st.blank, st.eot], begin),
+             SuppressTokensLogitsProcessor(list(suppress)),
+             WhisperTimeStampLogitsProcessor(gc, begin)]
+    sample = np.sort(np.random.default_rng(2024).choice(d.n_vocab, TURBO_SUBSET, replace=False)).astype(np.int32)
+    seq = list(prompt)
+    ids, lps, full, full_steps, lse, sub_i, sub_v, margins = [], [], [], [], [], [], [], []
+    sum_lp = 0.0
+    while True:
+        raw = lg.float().numpy()
+        k = len(lse)
+        if k < n_full_first or (full_every and k % full_every == 0):
+            full.append(raw.copy())
+            full_steps.append(k)
+        lse.append(float(torch.logsumexp(lg, -1)))
+        t32 = np.argsort(-raw, kind="stable")[:32].astype(np.int32)
+        sub_i.append(np.concatenate([t32, sample]))
+        sub_v.append(raw[sub_i[-1]])
+        x = lg[None].clone().float()
+        for p in procs:
+            x = p(torch.tensor([seq]), x)
+        lsm = torch.log_softmax(x.double(), -1)[0]
+        top2 = torch.topk(x[0], 2).values
+        margins.append(float(top2[0] - top2[1]))
+        nxt = int(torch.argmax(x[0]))
+        sum_lp += float(lsm[nxt])
+        lps.append(float(lsm[nxt]))
+        if nxt == st.eot:
+            break
+        ids.append(nxt)
+        seq.append(nxt)
+        if len(seq) >= d.n_text_ctx:
+            break
+        lg, past = step([nxt], past)
+    return dict(sot_logits=sot_logits, full_logits=np.stack(full), full_steps=np.array(full_steps, np.int32),
+                lse=np.array(lse), sub_ids=np.stack(sub_i), sub_vals=np.stack(sub_v), ids=np.array(ids, np.int32),
+                logprobs=np.array(lps), margins=np.array(margins), language=np.int32(lang),
+                no_speech_prob=np.float64(nsp), sum_logprob=np.float64(sum_lp))
+
+
+def gen_turbo_text(out):
+    """whisper-large-v3-turbo, text weights (TEXT_SEED, TEXT_AMP), three 30 s clips:
+    greedy to 448 positions each (full logits at the first 4 steps and every 32nd for
+    the first clip, at the first 4 for the others), and beam 5 on the first clip."""
+    from oracle import decode as odec
+
+    d = D.LARGE_V3_TURBO
+    st = D.SpecialTokens.for_vocab(d.n_vocab)
+    w = weights.random_weights(d, seed=TEXT_SEED, text_pos=TEXT_AMP)
+    model = build_model(d, w)
+    del w
+    store, meta = {}, {"seed": TEXT_SEED, "text_pos": TEXT_AMP, "clips": list(TEXT_CLIPS), "per_clip": {}}
+    encs = {}
+    for ci, (name, make) in enumerate(TEXT_CLIPS.items()):
+        mel = fe_mel(make(), d.n_mels)[:, :3000]
+        with torch.no_grad():
+            enc = model.model.encoder(input_features=torch.from_numpy(mel)[None]).last_hidden_state
+        encs[name] = enc
+        g = greedy_golden(model, d, enc, TURBO_FULL_STRIDE if ci == 0 else None)
+        e = enc[0].numpy()
+        g["enc_rownorm"] = np.linalg.norm(e.astype(np.float64), axis=1)
+        for k, v in g.items():
+            store[f"{name}/{k}"] = v
+        ids = g["ids"]
+        meta["per_clip"][name] = {"n_ids": int(len(ids)), "distinct_ids": int(len(set(ids.tolist()))),
+                                  "timestamp_ids": int((ids >= st.timestamp_begin).sum()),
+                                  "min_top2_margin": float(g["margins"].min()),
+                                  "p1_top2_margin": float(np.percentile(g["margins"], 1)),
+                                  "logit_std": float(np.std(g["full_logits"][0]))}
+        print("turbo text", name, meta["per_clip"][name], "first", ids[:10].tolist())
+    sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+    r = odec.beam_from_encoder(_HFStepper(model, encs["chirp0"]), None, st,
+                               opts=odec.DecodeOptions(suppress_tokens=sup, max_length=TURBO_BEAM_MAX_LEN),
+                               beam=odec.BeamOptions(beam_size=5))
+    store["beam5/ids"] = np.array(r.tokens, np.int32)
+    store["beam5/sum_logprob"] = np.float64(r.sum_logprob)
+    store["beam5/language"] = np.int32(r.language)
+    store["beam5/no_speech_prob"] = np.float64(r.no_speech_prob)
+    store["beam5/max_length"] = np.int32(TURBO_BEAM_MAX_LEN)
+    meta["beam5"] = {"clip": "chirp0", "n_ids": len(r.tokens), "distinct_ids": len(set(r.tokens)),
+                     "max_length": TURBO_BEAM_MAX_LEN}
+    print("turbo text beam5", meta["beam5"], "first", r.tokens[:10])
+    np.savez_compressed(os.path.join(out, "turbo_text.npz"), **store)
+    return meta
+
+
+def gen_tiny_text(out):
+    """tiny dims, text weights: greedy ids of one 30 s clip (the CPU oracle and the
+    GPU are both held to them)."""
+    d = D.TINY_TEST
+    w = weights.random_weights(d, seed=TEXT_SEED, text_pos=TINY_TEXT_AMP)
+    model = build_model(d, w)
+    mel = fe_mel(synth.chirp_clip(3, 30.0), d.n_mels)[:, :3000]
+    with torch.no_grad():
+        enc = model.model.encoder(input_features=torch.from_numpy(mel)[None]).last_hidden_state
+    g = greedy_golden(model, d, enc, None, n_full_first=8)
+    g["mel"] = mel
+    np.savez_compressed(os.path.join(out, "tiny_text.npz"), **g)
+    ids = g["ids"]
+    meta = {"seed": TEXT_SEED, "text_pos": TINY_TEXT_AMP, "clip": "chirp_clip(3, 30 s)", "n_ids": int(len(ids)),
+            "distinct_ids": int(len(set(ids.tolist()))), "min_top2_margin": float(g["margins"].min())}
+    print("tiny text", meta, "first", ids[:10].tolist())
+    return meta
+
+
 def gen_logits_rules(out):
     """Crafted token histories through transformers' Whisper processors."""
     st = D.SpecialTokens.for_vocab(51866)
@@ -379,7 +519,8 @@ def gen_logits_rules(out):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "tests", "golden"))
-    ap.add_argument("--only", default=None, help="comma list of: mel,rules,tiny,turbo_layer,turbo,turbo_beam")
+    ap.add_argument("--only", default=None,
+                    help="comma list of: mel,rules,tiny,turbo_layer,turbo,turbo_beam,tiny_text,turbo_text")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     torch.manual_seed(0)
@@ -387,7 +528,8 @@ def main():
     meta = json.load(open(mp)) if os.path.exists(mp) else {}
     meta.update({"generator": "tools/make_golden.py", "transformers": __import__("transformers").__version__,
                  "torch": torch.__version__})
-    only = set(a.only.split(",")) if a.only else {"mel", "rules", "tiny", "turbo_layer", "turbo", "turbo_beam"}
+    only = set(a.only.split(",")) if a.only else {"mel", "rules", "tiny", "turbo_layer", "turbo", "turbo_beam",
+                                                 "tiny_text", "turbo_text"}
     if "mel" in only:
         meta["mel"] = gen_mel(a.out)
     if "rules" in only:
@@ -400,6 +542,10 @@ def main():
         meta["turbo"] = gen_turbo(a.out)
     if "turbo_beam" in only:
         meta["turbo_beam"] = gen_turbo_beam(a.out)
+    if "tiny_text" in only:
+        meta["tiny_text"] = gen_tiny_text(a.out)
+    if "turbo_text" in only:
+        meta["turbo_text"] = gen_turbo_text(a.out)
     with open(os.path.join(a.out, "meta.json"), "w") as fh:
         json.dump(meta, fh, indent=1)
 

@@ -765,7 +765,7 @@ __global__ __launch_bounds__(256) void dec_xattn_mfma_kernel(const float* __rest
 // part == nullptr the embedding entry x[b] = tok_emb[tok[b]] + pos_emb[pos].  The
 // arithmetic is resln_rows (resln.h), shared with the fused GEMM prologue.
 __global__ __launch_bounds__(256) void dec_resid_ln_kernel(ResLnArgs A, h16* __restrict__ y, int64_t lo_off) {
-    __shared__ float red[2 * 4];
+    __shared__ __attribute__((aligned(16))) float red[resln_scratch(1, 1280)];
     const int b = blockIdx.x;
     resln_rows<1, 8>(A, b, 1, true, red,
                   [&](int, int c, float v) { split_h16(v, y, y + lo_off, (int64_t)b * A.D + c); });

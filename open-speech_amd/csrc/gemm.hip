@@ -1294,7 +1294,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL ? 4 : 1
     constexpr int APR = PRO == PRO_GELU ? GELU_ROWS : PRO == PRO_RESLN ? PRO_ROWS : 1;  // image rows
     constexpr int APS = PRO == PRO_GELU ? GELU_KC + 8 : PRO == PRO_RESLN ? PRO_STRIDE : 8;
     __shared__ __attribute__((aligned(16))) h16 Ap[PRO ? 2 : 1][APR][APS];
-    __shared__ float pred[PRO ? 2 * PRO_ROWS * 4 : 1];
+    __shared__ __attribute__((aligned(16))) float pred[PRO ? resln_scratch(PRO_ROWS, 1280) : 1];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
     if (g.pair_rows) {

@@ -2,9 +2,14 @@
 // decode-graph launches: T host threads, each with its own stream,
 // capture a graph of K small kernel launches, instantiate it and replay it R times;
 // with mode 1 one extra thread keeps capturing and instantiating NEW graphs meanwhile
-// (what a lane does on the first call of a new decode-options key).  No libosw code.
+// (what a lane does on the first call of a new decode-options key).  Mode 2 (VERDICT r4
+// item 7, the state gpurun_out/r04_k/stream_probe_prof.txt:110-116 shows) adds a thread
+// that launches kernels EAGERLY on its own stream, as osw_encode_windows does for an
+// encoder below the baton threshold (a pageable H2D copy of the window table, ~300
+// launches, an event record), while the capturing thread replays each freshly
+// instantiated graph a few times.  No libosw code.
 // Build: hipcc --offload-arch=gfx950 -O2 -o tools/graph_prof_repro tools/graph_prof_repro.hip -lpthread
-// Run:   tools/graph_prof_repro [threads=3] [replays=300] [mode=1]
+// Run:   tools/graph_prof_repro [threads=3] [replays=300] [mode=1|2]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -60,7 +65,29 @@ int main(int argc, char** argv) {
             CK(hipFree(buf));
             CK(hipStreamDestroy(s));
         });
-    if (mode == 1)
+    if (mode == 2)
+        th.emplace_back([=] {  // a sibling lane encoding eagerly beside the replays
+            hipStream_t s;
+            hipEvent_t ev;
+            float* buf;
+            int* win;
+            CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+            CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            CK(hipMalloc(&buf, n * sizeof(float)));
+            CK(hipMalloc(&win, 64 * sizeof(int)));
+            std::vector<int> hw(64, 1);
+            for (int r = 0; r < R / 4; ++r) {
+                CK(hipMemcpyAsync(win, hw.data(), hw.size() * sizeof(int), hipMemcpyHostToDevice, s));
+                for (int i = 0; i < 300; ++i) step_kernel<<<(n + 255) / 256, 256, 0, s>>>(buf, n, 0.5f);
+                CK(hipEventRecord(ev, s));
+                CK(hipEventSynchronize(ev));
+            }
+            CK(hipFree(win));
+            CK(hipFree(buf));
+            CK(hipEventDestroy(ev));
+            CK(hipStreamDestroy(s));
+        });
+    if (mode >= 1)
         th.emplace_back([=] {  // a lane meeting new decode-options keys: capture after capture
             hipStream_t s;
             float* buf;
@@ -68,7 +95,7 @@ int main(int argc, char** argv) {
             CK(hipMalloc(&buf, n * sizeof(float)));
             for (int r = 0; r < R / 4; ++r) {
                 hipGraphExec_t ge = capture(s, buf, n, 8 + r % 8);
-                CK(hipGraphLaunch(ge, s));
+                for (int k = 0; k < (mode == 2 ? 4 : 1); ++k) CK(hipGraphLaunch(ge, s));
                 CK(hipStreamSynchronize(s));
                 CK(hipGraphExecDestroy(ge));
             }

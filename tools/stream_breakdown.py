@@ -61,10 +61,10 @@ for nm in ("log_mel", "encode", "decode"):
 orig_submit = R.BatchRunner.submit_req
 
 
-def submit_req(self, r, exclude=None):
+def submit_req(self, r, *a, **k):
     if not hasattr(r, "_t_sub"):
         r._t_sub = time.perf_counter()
-    return orig_submit(self, r, exclude)
+    return orig_submit(self, r, *a, **k)
 
 
 R.BatchRunner.submit_req = submit_req

@@ -134,14 +134,9 @@ class HipWhisperBackend:
                 for e in engines:
                     e.close()
                 raise
-            # pipelined lanes (runner.py): a lone free lane takes half of what is queued and
-            # every encoder takes the sibling lanes' encoder baton, so one batch encodes
-            # while another decodes
+            # pipelined lanes (runner.py): the lanes of a GPU take turns on the encoder, so
+            # one batch encodes while the others decode
             split = os.environ.get("STT_HIP_SPLIT", "1") != "0"
-            if split and "OSW_BATON_MIN_WINDOWS" not in os.environ:
-                for e in engines:
-                    if hasattr(e, "set_encoder_baton_min"):
-                        e.set_encoder_baton_min(0)
             tok = WhisperTokenizer(src.dims.n_vocab, src.tokenizer_json)
             runner = BatchRunner(engines, tok, max_wait_ms=wait_ms, gap_ms=gap_ms, split=split)
             self._models[model_id] = _Model(src, runner, tok, engines)

@@ -10,14 +10,16 @@ each) pull batches from that queue: a free lane that finds the queue non-empty w
 for company (at most ``max_wait_ms`` after the oldest request, ``gap_ms`` after the
 latest), takes up to ``max_batch`` requests and runs them as one batched seek loop.
 
-Pipelining (``split``): when no other lane of the GPU is running a batch, the lane
-takes only half of what is queued (rounded up) and leaves the rest to the next free
-lane, which takes it at once.  The sibling lanes' encoders are serialised on the GPU
-(the encoder baton, ``osw_set_encoder_baton_min``), so the second batch encodes while
-the first decodes.  Under the streaming pool's closed loop (4 calls in flight, each
-session waiting for its call) this turns lock-step batches of 4 — encode 4, decode
-4, nothing overlapping — into two staggered batches of 2 whose encoder and decoder
-phases overlap.  With a deep queue (REST load) both halves are ``max_batch`` anyway.
+Pipelining (``split``): a GPU runs one encoder at a time (a lane's ``engine.encode`` is
+synchronous, and it is tracked per GPU).  A free lane that finds requests queued while
+another lane of its GPU is encoding waits for that encoder to finish and then takes
+everything queued (up to ``max_batch``); when the encoder is idle and no other lane is
+running a batch, it takes half of the queue (rounded up) and leaves the rest to the next
+free lane, which then waits for this lane's encoder.  Under the streaming pool's closed
+loop (4 calls in flight, each session waiting for its call) this turns lock-step batches
+of 4 — encode 4, decode 4, nothing overlapping — into staggered batches that take turns
+on the encoder while the other batches decode.  With a deep queue (REST load) the
+batches are ``max_batch`` anyway.
 
 A lane whose GPU fails marks every lane of that GPU dead, moves the GPU's queued
 requests to the other GPUs and re-queues there the requests of its batch that are
@@ -54,6 +56,7 @@ class _DevQueue:
         self.cv = threading.Condition()
         self.lanes: list = []
         self.collecting = False     # a lane is waiting for company for its batch
+        self.encoding = 0           # lanes inside engine.encode (synchronous) on this GPU
         self.alive = True
         self.closing = False
 
@@ -67,10 +70,30 @@ class _DevQueue:
             self.cv.notify_all()
 
 
+class _LaneEngine:
+    """The lane's engine, with its encoder calls counted on the GPU's queue."""
+
+    def __init__(self, engine, dq: _DevQueue):
+        self._e, self._dq = engine, dq
+
+    def __getattr__(self, k):
+        return getattr(self._e, k)
+
+    def encode(self, windows):
+        with self._dq.cv:
+            self._dq.encoding += 1
+        try:
+            return self._e.encode(windows)
+        finally:
+            with self._dq.cv:
+                self._dq.encoding -= 1
+                self._dq.cv.notify_all()
+
+
 class _Worker(threading.Thread):
     def __init__(self, pool: "BatchRunner", engine, idx: int, dq: _DevQueue):
         super().__init__(daemon=True, name=f"osw-lane-{idx}")
-        self.pool, self.engine, self.idx, self.dq = pool, engine, idx, dq
+        self.pool, self.engine, self.idx, self.dq = pool, _LaneEngine(engine, dq), idx, dq
         self.alive = True
         self.inflight = 0
 
@@ -104,12 +127,21 @@ class _Worker(threading.Thread):
                     if left <= 0:
                         break
                     dq.cv.wait(timeout=left)
+                if pool.split:
+                    # another lane's encoder is running: wait for it (bounded), then take
+                    # everything that queued meanwhile
+                    end = time.monotonic() + pool.max_pace_ms / 1000.0
+                    while dq.encoding and not dq.closing and self.alive:
+                        left = end - time.monotonic()
+                        if left <= 0:
+                            break
+                        dq.cv.wait(timeout=left)
                 if dq.closing or not self.alive or not dq.items:
                     return None if (dq.closing or not self.alive) else []
                 k = min(cap, len(dq.items))
                 others_busy = any(w.inflight for w in dq.lanes if w is not self)
                 idle_sibling = any(w.alive and not w.inflight for w in dq.lanes if w is not self)
-                if pool.split and not others_busy and idle_sibling:
+                if pool.split and not others_busy and idle_sibling and not dq.encoding:
                     k = min(k, (len(dq.items) + 1) // 2)
                 batch = [dq.items.popleft() for _ in range(k)]
                 self.inflight = len(batch)
@@ -157,11 +189,12 @@ class _Worker(threading.Thread):
 
 class BatchRunner:
     def __init__(self, engines: list, tokenizer: WhisperTokenizer, max_wait_ms: float = 5.0,
-                 gap_ms: float | None = None, split: bool = True):
+                 gap_ms: float | None = None, split: bool = True, max_pace_ms: float = 100.0):
         self.tokenizer = tokenizer
         self.max_wait_ms = max_wait_ms
         self.gap_ms = gap_ms
         self.split = split
+        self.max_pace_ms = max_pace_ms
         self._sup_cache: dict = {}
         self._lock = threading.Lock()
         self.queues: list[_DevQueue] = []
@@ -245,6 +278,6 @@ class BatchRunner:
                     r.fut.set_exception(RuntimeError("runner closed"))
             q.items.clear()
         for w in self.workers:
-            close = getattr(w.engine, "close", None)
+            close = getattr(w.engine._e, "close", None)
             if close:
                 close()

@@ -440,3 +440,44 @@ def test_split_pipelines_lanes(split, want):
         assert sorted(b for e in es for b in e.batches) == want
     finally:
         runner.close()
+
+
+def test_lanes_take_turns_on_the_encoder():
+    """Pipelined lanes: while one lane encodes, a free lane waits for that encoder and
+    then takes everything that queued meanwhile (one batch), instead of starting a
+    one-request batch whose encoder would only queue behind it."""
+    from concurrent.futures import Future
+    from open_speech_amd.runner import BatchRunner, _Req
+    from open_speech_amd.segments import TranscribeOptions
+    from open_speech_amd.tokenizer import WhisperTokenizer
+
+    class Eng(FakeEngine):
+        def __init__(self):
+            super().__init__(D.MICRO_TEST, 0, 8,
+                             lambda w, i, p, l: WindowOutput([TB, 1000, TB + 50], -1.0, 0.01, ST.first_lang))
+            self.device = 0
+            self.enc_windows = []
+
+        def encode(self, wins):
+            self.enc_windows.append(len(wins))
+            time.sleep(0.15)
+            return super().encode(wins)
+
+        def decode(self, n, cfg, prefix=None, dump_steps=0, languages=None):
+            time.sleep(0.1)   # lane A still decodes when lane B takes its batch
+            return super().decode(n, cfg, prefix, dump_steps, languages)
+
+    es = [Eng(), Eng(), Eng()]
+    runner = BatchRunner(es, WhisperTokenizer(51866), max_wait_ms=500, gap_ms=5, split=True)
+    try:
+        opts = TranscribeOptions(beam_size=1, language="en")
+        reqs = [_Req(synth.chirp_clip(i, 3.0), opts, Future()) for i in range(5)]
+        runner.submit_req(reqs[0])
+        time.sleep(0.05)                  # lane A is encoding request 0
+        for r in reqs[1:]:
+            runner.submit_req(r)
+        for r in reqs:
+            assert r.fut.result(timeout=30).segments
+        assert sorted(n for e in es for n in e.enc_windows) == [1, 4]
+    finally:
+        runner.close()

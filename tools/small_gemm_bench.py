@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Encoder GEMM shapes at 1, 2, 4 and 8 windows (M = 1500 w): every tile variant timed
 (debug entry, fp32 out) and checked bit-identical against the 128 double-buffered tile.
-variants: 1 = 128 tile, 4 = 8-phase 256, 6 = 64 ring, 7 = 64 tile, 11 = 128 ring."""
+variants: 1 = 128 tile, 4 = 8-phase 256, 6 = 64 ring, 7 = 64 tile, 11 = 128 ring,
+14 = 128 tile with software-pipelined LDS reads.  usage: small_gemm_bench.py [windows] [variants] [gemms]"""
 import json
 import os
 import sys
@@ -20,14 +21,17 @@ d = D.WhisperDims(n_mels=80, n_audio_state=128, n_audio_head=2, n_audio_layer=1,
 eng = WhisperEngine(d, device=0, max_batch=1)
 rng = np.random.default_rng(0)
 wins = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [1, 4]
+variants = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 6, 7, 11, 4, 14]
+gemms = sys.argv[3].split(",") if len(sys.argv) > 3 else ["qkv", "o", "fc1", "fc2", "xkv"]
+shapes = {"qkv": (3840, 1280), "o": (1280, 1280), "fc1": (5120, 1280), "fc2": (1280, 5120), "xkv": (10240, 1280)}
 for w in wins:
     M = 1500 * w
-    for name, N, K in (("qkv", 3840, 1280), ("o", 1280, 1280), ("fc1", 5120, 1280), ("fc2", 1280, 5120),
-                       ("xkv", 10240, 1280)):
+    for name in gemms:
+        N, K = shapes[name]
         A = rng.uniform(-1, 1, (M, K)).astype(np.float16)
         W = rng.uniform(-1, 1, (N, K)).astype(np.float16)
         ref = None
-        for v in (1, 6, 7, 11, 4):
+        for v in variants:
             C, ms = eng.debug_gemm(A, W, v, iters=10)
             if ref is None:
                 ref = C

@@ -162,6 +162,7 @@ void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s);  // 0 a
 // M <= 64, K % 128 == 0; `part` needs skinny_ksplit(N,K)*M*N floats
 void launch_gemm_skinny(const GemmArgs& g, float* part, hipStream_t s);
 int skinny_ksplit(int N, int K);
+void prepare_gemm_kernels();  // every GEMM kernel's dynamic-LDS attribute, once (osw_create)
 int tiled_ksplit(int M, int N, int K);
 void launch_gemm_tiled_partial(const GemmArgs& g, float* part, int ks, hipStream_t s);
 int launch_gemm_skinny_partial(const GemmArgs& g, float* part, hipStream_t s);

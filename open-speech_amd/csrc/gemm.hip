@@ -18,6 +18,8 @@
 #include "resln.h"
 
 #include <cstdlib>
+#include <mutex>
+#include <set>
 #include <stdexcept>
 
 namespace osw {
@@ -26,6 +28,18 @@ namespace {
 #include "select.h"
 
 constexpr int BM = 128, BN = 128, BK = 64, NTHR = 256;
+
+// Dynamic-LDS limits are set once per kernel, before its first launch, under a lock, and
+// all of them when a context is created (prepare_gemm_kernels): a lazily set attribute
+// (a racy `static bool` per launcher before round 5) ran hipFuncSetAttribute in whichever
+// lane thread launched the kernel first, concurrently with other lanes' launches and
+// graph replays.
+void set_lds_once(const void* kernel, int bytes) {
+    static std::mutex mu;
+    static std::set<const void*> done;
+    std::lock_guard<std::mutex> lk(mu);
+    if (done.insert(kernel).second) (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
 
 // EPI_HEADS: the cross-K/V slot of window b of this GEMM (row refill encodes new windows
 // into the slots of finished ones)
@@ -501,12 +515,8 @@ int choose_band(const GemmArgs& g) {
 
 template <int EPI>
 void launch256(const GemmArgs& g0, hipStream_t s) {
-    static bool attr = false;
     constexpr int lds = EPI_LDS > 2 * 2 * GB * BK * 2 ? EPI_LDS : 2 * 2 * GB * BK * 2;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        attr = true;
-    }
+    set_lds_once((const void*)gemm256_kernel<EPI>, lds);
     GemmArgs g = g0;
     g.band = choose_band(g);
     const int nwg = ((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
@@ -856,13 +866,8 @@ __global__ __launch_bounds__(GNT, 1) void gemm8p_kernel(GemmArgs g) {
 
 template <int EPI, int DBG = 0>
 void launch8p(const GemmArgs& g0, hipStream_t s) {
-    static bool attr = false;
     constexpr int lds = EPI_LDS > 8 * HT * 2 ? EPI_LDS : 8 * HT * 2;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gemm8p_kernel<EPI, DBG>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  lds);
-        attr = true;
-    }
+    set_lds_once((const void*)gemm8p_kernel<EPI, DBG>, lds);
     GemmArgs g = g0;
     g.band = choose_band(g);
     // the next tile's first K-tile staged during the epilogue: only the head-major qkv
@@ -1166,24 +1171,14 @@ __global__ __launch_bounds__(NTHR, 1) void gemm128_pipe_kernel(GemmArgs g) {
 
 template <int EPI>
 void launch_pipe128(const GemmArgs& g, hipStream_t s) {
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gemm128_pipe_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  R128_LDS);
-        attr = true;
-    }
+    set_lds_once((const void*)gemm128_pipe_kernel<EPI>, R128_LDS);
     const int nwg = ((g.N + 127) / 128) * ((g.M + 127) / 128);
     gemm128_pipe_kernel<EPI><<<nwg, NTHR, R128_LDS, s>>>(g);
 }
 
 template <int EPI>
 void launch_ring128(const GemmArgs& g, hipStream_t s) {
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gemm128_ring_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  R128_LDS);
-        attr = true;
-    }
+    set_lds_once((const void*)gemm128_ring_kernel<EPI>, R128_LDS);
     const int nwg = ((g.N + 127) / 128) * ((g.M + 127) / 128);
     gemm128_ring_kernel<EPI><<<nwg, NTHR, R128_LDS, s>>>(g);
 }
@@ -1859,12 +1854,8 @@ __global__ __launch_bounds__(WN * 2, WN == WBN ? 2 : 1) void gemm_wide_kernel(Ge
 
 template <bool LO>
 void launch_wide256(const GemmArgs& g, int ks, hipStream_t s) {
-    static bool attr = false;
     constexpr int lds = wide_lds<256>(LO);
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gemm_wide_kernel<LO, 256>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        attr = true;
-    }
+    set_lds_once((const void*)gemm_wide_kernel<LO, 256>, lds);
     gemm_wide_kernel<LO, 256><<<dim3((g.N + 255) / 256, (g.M + WBM - 1) / WBM, ks), 512, lds, s>>>(g);
 }
 
@@ -2053,6 +2044,33 @@ void launch_gemm_skinny(const GemmArgs& g, float* part, hipStream_t s) {
         case EPI_F32: skinny_mt<EPI_F32>(g, ks, part, s); break;
         default: break;  // other epilogues are encoder-only
     }
+}
+
+// every dynamic-LDS attribute of the GEMM kernels, set once (osw_create calls it)
+void prepare_gemm_kernels() {
+    static std::once_flag once;
+    std::call_once(once, [] {
+        constexpr int l256 = EPI_LDS > 2 * 2 * GB * BK * 2 ? EPI_LDS : 2 * 2 * GB * BK * 2;
+        constexpr int l8p = EPI_LDS > 8 * HT * 2 ? EPI_LDS : 8 * HT * 2;
+        auto each = [&](auto e) {
+            constexpr int E = decltype(e)::value;
+            set_lds_once((const void*)gemm256_kernel<E>, l256);
+            set_lds_once((const void*)gemm8p_kernel<E, 0>, l8p);
+            set_lds_once((const void*)gemm128_ring_kernel<E>, R128_LDS);
+            set_lds_once((const void*)gemm128_pipe_kernel<E>, R128_LDS);
+        };
+        each(std::integral_constant<int, EPI_F16>{});
+        each(std::integral_constant<int, EPI_F16_GELU>{});
+        each(std::integral_constant<int, EPI_F32_RESID>{});
+        each(std::integral_constant<int, EPI_F32_GELU_POS>{});
+        each(std::integral_constant<int, EPI_F32>{});
+        each(std::integral_constant<int, EPI_HEADS>{});
+        set_lds_once((const void*)gemm8p_kernel<EPI_F32, 1>, l8p);
+        set_lds_once((const void*)gemm8p_kernel<EPI_F16, 2>, l8p);
+        set_lds_once((const void*)gemm8p_kernel<EPI_F16_GELU, 2>, l8p);
+        set_lds_once((const void*)gemm_wide_kernel<true, 256>, wide_lds<256>(true));
+        set_lds_once((const void*)gemm_wide_kernel<false, 256>, wide_lds<256>(false));
+    });
 }
 
 void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s);

@@ -1511,6 +1511,7 @@ int osw_create(const osw_dims* dims, int32_t device, int32_t max_batch, osw_ctx*
         // OSW_BATON_MIN_WINDOWS=n: encoders below n windows skip the baton (0: never skip)
         if (const char* e = std::getenv("OSW_BATON_MIN_WINDOWS")) c->baton_min = atoi(e);
         DeviceScope dev_scope_((device));
+        prepare_gemm_kernels();  // no kernel attribute is set lazily beside other lanes' launches
         make_streams(c);
         const char* eb = std::getenv("OSW_ENC_BATON");
         if (!eb || eb[0] != '0') {

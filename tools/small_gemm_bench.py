@@ -20,9 +20,9 @@ d = D.WhisperDims(n_mels=80, n_audio_state=128, n_audio_head=2, n_audio_layer=1,
                   n_text_layer=1)
 eng = WhisperEngine(d, device=0, max_batch=1)
 rng = np.random.default_rng(0)
-wins = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [1, 4]
-variants = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 6, 7, 11, 4, 14]
-gemms = sys.argv[3].split(",") if len(sys.argv) > 3 else ["qkv", "o", "fc1", "fc2", "xkv"]
+wins = [int(x) for x in sys.argv[1].replace(":", ",").split(",")] if len(sys.argv) > 1 else [1, 4]
+variants = [int(x) for x in sys.argv[2].replace(":", ",").split(",")] if len(sys.argv) > 2 else [1, 6, 7, 11, 4, 14]
+gemms = sys.argv[3].replace(":", ",").split(",") if len(sys.argv) > 3 else ["qkv", "o", "fc1", "fc2", "xkv"]
 shapes = {"qkv": (3840, 1280), "o": (1280, 1280), "fc1": (5120, 1280), "fc2": (1280, 5120), "xkv": (10240, 1280)}
 for w in wins:
     M = 1500 * w

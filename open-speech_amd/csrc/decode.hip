@@ -1070,21 +1070,24 @@ __device__ __forceinline__ ArgMax block_amax(ArgMax a, ArgMax* red) {
 
 // grid windows, 256 threads: merge the candidates, register finished hypotheses,
 // pick the surviving beams and reorder their tokens / ancestry / state.
+// KM: the largest beam the LDS arrays hold (5, the reference's beam_size: 24 KiB, so the
+// workgroup fits beside another lane's 128-KiB encoder workgroup; 8: 45 KiB)
+template <int KM>
 __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* __restrict__ pos_ptr,
                                                           SelState* __restrict__ st, const SelPart* __restrict__ parts,
                                                           const BeamCand* __restrict__ cand, int* __restrict__ seq,
                                                           int* __restrict__ anc, int ctx, BeamWin* __restrict__ bwin,
                                                           int* __restrict__ best_tok, int* __restrict__ cur_tok,
                                                           int max_tokens) {
-    constexpr int MAXC = MAX_BEAM * BEAM_SLICES * MAXK2;
+    constexpr int MAXC = KM * BEAM_SLICES * 2 * KM;
     __shared__ float cs[MAXC];
     __shared__ int ci[MAXC];
-    __shared__ BeamCand top[2 * MAX_BEAM];
+    __shared__ BeamCand top[2 * KM];
     __shared__ ArgMax red[4];
-    __shared__ int lseq[MAX_BEAM][448];
-    __shared__ int lanc[MAX_BEAM][448];
-    __shared__ SelState lst[MAX_BEAM];
-    __shared__ int choose[MAX_BEAM], fin, best_src, best_extra, improved;
+    __shared__ int lseq[KM][448];
+    __shared__ int lanc[KM][448];
+    __shared__ SelState lst[KM];
+    __shared__ int choose[KM], fin, best_src, best_extra, improved;
     const int w = blockIdx.x, tid = threadIdx.x, K = P.beam, K2 = 2 * K;
     const int r0 = w * K;
     const int step = *pos_ptr;
@@ -1096,8 +1099,8 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
     constexpr int LB = 8;
     // per row: lse over the allowed tokens, over the allowed timestamps, and the
     // timestamp-mass rule (the row's 16 slice statistics in fixed order)
-    __shared__ float rlse[MAX_BEAM], rsum[MAX_BEAM];
-    __shared__ int rts[MAX_BEAM];
+    __shared__ float rlse[KM], rsum[KM];
+    __shared__ int rts[KM];
     if (tid < K) {
         rsum[tid] = st[r0 + tid].sum_lp;
         const SelPart r = combine_parts<false>(parts + (int64_t)(r0 + tid) * SEL_SPLIT);
@@ -1252,6 +1255,7 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
 // grid windows: the per-window merge / finish / reorder, then an arrival count over
 // the windows; the last one advances the device step counter (every window read it
 // at its start), so beam steps need no separate bump launch.
+template <int KM>
 __global__ __launch_bounds__(256) void beam_update_kernel(SelParams P, int* __restrict__ pos_ptr,
                                                           SelState* __restrict__ st, const SelPart* __restrict__ parts,
                                                           const BeamCand* __restrict__ cand, int* __restrict__ seq,
@@ -1259,7 +1263,7 @@ __global__ __launch_bounds__(256) void beam_update_kernel(SelParams P, int* __re
                                                           int* __restrict__ best_tok, int* __restrict__ cur_tok,
                                                           int max_tokens, int* __restrict__ arrive) {
     const int step = *pos_ptr;
-    beam_update_body(P, pos_ptr, st, parts, cand, seq, anc, ctx, bwin, best_tok, cur_tok, max_tokens);
+    beam_update_body<KM>(P, pos_ptr, st, parts, cand, seq, anc, ctx, bwin, best_tok, cur_tok, max_tokens);
     __syncthreads();
     if (threadIdx.x != 0) return;
     __builtin_amdgcn_s_waitcnt(0);
@@ -1406,8 +1410,13 @@ void launch_select(const float* logits, int rows, int* pos, const SelParams& P, 
 void launch_beam(const float* logits, int windows, int* pos, const SelParams& P, const unsigned* supmask,
                  SelState* st, const void* sel_parts, void* cand, int* seq, int* anc, int ctx, BeamWin* bw,
                  int* best_tok, int* cur_tok, int max_tokens, int* arrive, hipStream_t s) {
-    beam_update_kernel<<<windows, 256, 0, s>>>(P, pos, st, (const SelPart*)sel_parts, (const BeamCand*)cand, seq,
-                                                anc, ctx, bw, best_tok, cur_tok, max_tokens, arrive);
+    if (P.beam <= 5)
+        beam_update_kernel<5><<<windows, 256, 0, s>>>(P, pos, st, (const SelPart*)sel_parts, (const BeamCand*)cand, seq,
+                                                      anc, ctx, bw, best_tok, cur_tok, max_tokens, arrive);
+    else
+        beam_update_kernel<MAX_BEAM><<<windows, 256, 0, s>>>(P, pos, st, (const SelPart*)sel_parts,
+                                                             (const BeamCand*)cand, seq, anc, ctx, bw, best_tok, cur_tok,
+                                                             max_tokens, arrive);
 }
 
 void launch_count_done(const SelState* st, int rows, int* out, hipStream_t s) {

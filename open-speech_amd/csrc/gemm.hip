@@ -28,6 +28,9 @@ namespace {
 #include "select.h"
 
 constexpr int BM = 128, BN = 128, BK = 64, NTHR = 256;
+#ifndef OSW_SKINNY_CK1
+#define OSW_SKINNY_CK1 4  // k32 steps per chunk of the 16-row hi/lo skinny GEMM (A/B builds: 8)
+#endif
 
 // Dynamic-LDS limits are set once per kernel, before its first launch, under a lock, and
 // all of them when a context is created (prepare_gemm_kernels): a lazily set attribute
@@ -1020,162 +1023,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm128_ring_kernel(GemmArgs g) {
     }
 }
 
-// The 128x128 tile with its LDS reads software-pipelined (round 5): gemm128_ring_kernel's
-// tile, waves, ring and staging, but every 64-deep K step runs as
-//     read fragments of k32 half 1 | MFMAs of half 0 | wait for tile kt+1, barrier |
-//     MFMAs of half 1 with tile kt+4's LDS-DMA into slot kt and the reads of tile kt+1's
-//     half 0 issued among them
-// so a half's ds_reads land while the other half's 16 MFMAs run (the ring kernel read both
-// halves' fragments and waited for them before each half, one wave per SIMD with nothing
-// to hide the LDS latency: fc2 at two windows 65 us = 29 % of the CU's MFMA rate), and the
-// next tile's LDS-DMA pieces are issued between the MFMAs.  One barrier per K step.  Same
-// MFMA chain per output element in the same K order: identical results.
-template <int EPI>
-__global__ __launch_bounds__(NTHR, 1) void gemm128_pipe_kernel(GemmArgs g) {
-    constexpr int TM = 128, PW = 4, FT = 4, WT = 64;
-    extern __shared__ __attribute__((aligned(16))) h16 smem[];  // [NS][A|W][128*64]
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int ntm = (g.M + TM - 1) / TM, ntn = (g.N + TM - 1) / TM, nwg = ntm * ntn;
-    const int bid = blockIdx.x, q = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
-    const int v = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + bid / 8;
-    const int m0 = (v % ntm) * TM, n0 = (v / ntm) * TM;
-    const h16* asrc[PW];
-    const h16* wsrc[PW];
-#pragma unroll
-    for (int i = 0; i < PW; ++i) {
-        const int r = (i * 4 + wave) * 8 + (lane >> 3);
-        const int c = swz(r, lane & 7);
-        asrc[i] = grp_row(g.A, min(m0 + r, g.M - 1), g.a_grp_rows, g.a_grp_stride, g.lda) + c * 8;
-        wsrc[i] = g.W + (int64_t)min(n0 + r, g.N - 1) * g.ldw + c * 8;
-    }
-    // LDS-DMA piece j (0..7) of a stage: A pieces 0..3, W pieces 4..7
-    auto piece = [&](int slot, int k0, int j) {
-        h16* base = smem + slot * R128_SLOT;
-        const int i = j & 3;
-        if (j < 4)
-            __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + k0), (OSW_LDS void*)(base + (i * 4 + wave) * 8 * BK),
-                                             16, 0, 0);
-        else
-            __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + k0),
-                                             (OSW_LDS void*)(base + TM * BK + (i * 4 + wave) * 8 * BK), 16, 0, 0);
-    };
-    const int wm = wave >> 1, wn = wave & 1;
-    f32x4 acc[FT][FT];
-#pragma unroll
-    for (int i = 0; i < FT; ++i)
-#pragma unroll
-        for (int j = 0; j < FT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int nk = g.K / BK;
-    int aoff[FT], boff[FT][2];
-    int aoffs[FT][2];
-#pragma unroll
-    for (int mi = 0; mi < FT; ++mi) {
-        const int row = wm * WT + mi * 16 + (lane & 15);
-        aoffs[mi][0] = row * BK + swz(row, lane >> 4) * 8;
-        aoffs[mi][1] = row * BK + swz(row, 4 + (lane >> 4)) * 8;
-    }
-#pragma unroll
-    for (int ni = 0; ni < FT; ++ni) {
-        const int row = wn * WT + ni * 16 + (lane & 15);
-        boff[ni][0] = TM * BK + row * BK + swz(row, lane >> 4) * 8;
-        boff[ni][1] = TM * BK + row * BK + swz(row, 4 + (lane >> 4)) * 8;
-    }
-    (void)aoff;
-    h16x8 fa[2][FT], fb[2][FT];
-    auto read = [&](int set, int slot, int half) {
-        const h16* b = smem + slot * R128_SLOT;
-#pragma unroll
-        for (int mi = 0; mi < FT; ++mi) fa[set][mi] = *(const h16x8*)&b[aoffs[mi][half]];
-#pragma unroll
-        for (int ni = 0; ni < FT; ++ni) fb[set][ni] = *(const h16x8*)&b[boff[ni][half]];
-    };
-    // the 16 MFMAs of one k32 half; `between(mi)` after the 4 MFMAs of row block mi
-    auto mfma = [&](int set, auto between) {
-#pragma unroll
-        for (int mi = 0; mi < FT; ++mi) {
-#pragma unroll
-            for (int ni = 0; ni < FT; ++ni)
-                acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[set][mi], fb[set][ni], acc[mi][ni], 0, 0, 0);
-            between(mi);
-        }
-    };
-    auto barrier = [] {
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-    };
-    // prologue: tiles 0 .. NS-1 in flight (every slot), tile 0 landed, its half 0 read;
-    // at K step kt tile kt+NS goes into slot kt once every wave has read it
-#pragma unroll
-    for (int t = 0; t < R128_NS; ++t)
-        if (t < nk)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) piece(t, t * BK, j);
-    {
-        const int ahead = min(R128_NS - 1, nk - 1);
-        if (ahead >= 3) wait_vmcnt<3 * 8>();
-        else if (ahead == 2) wait_vmcnt<2 * 8>();
-        else if (ahead == 1) wait_vmcnt<8>();
-        else wait_vmcnt<0>();
-    }
-    barrier();
-    read(0, 0, 0);
-    for (int kt = 0; kt < nk; ++kt) {
-        const int slot = kt % R128_NS;
-        read(1, slot, 1);
-        mfma(0, [](int) {});
-        if (kt + 1 < nk) {
-            // tile kt+1 landed once at most min(NS-2, nk-2-kt) younger stages are in flight
-            // (tiles kt+2 .. kt+NS-1; tile kt+NS is issued below)
-            const int ahead = min(R128_NS - 2, nk - 2 - kt);
-            if (ahead >= 2) wait_vmcnt<2 * 8>();
-            else if (ahead == 1) wait_vmcnt<8>();
-            else wait_vmcnt<0>();
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of slot kt are done
-            barrier();                                            // ... every wave's; tile kt+1 landed
-            // tile kt+NS's LDS-DMA pieces go out among the first 8 MFMAs of half 1, the
-            // reads of tile kt+1's half 0 after them (an LDS-DMA issued behind pending
-            // ds_reads would make the compiler drain them first), landing during the last 8
-            const bool st = kt + R128_NS < nk;
-            const int k0 = (kt + R128_NS) * BK;
-            mfma(1, [&](int mi) {
-                if (mi < 2 && st)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) piece(slot, k0, 4 * mi + j);
-                if (mi == 1) read(0, (kt + 1) % R128_NS, 0);
-            });
-        } else {
-            mfma(1, [](int) {});
-        }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __syncthreads();
-    if constexpr (EPI != EPI_F32) {
-        staged_epilogue_sq<EPI, TM>(g, acc, m0, n0, wm, wn, smem, threadIdx.x);
-    } else {  // (debug entry only) plain fp32 tile
-#pragma unroll
-        for (int mi = 0; mi < FT; ++mi)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int m = m0 + wm * WT + mi * 16 + (lane >> 4) * 4 + i;
-                if (m >= g.M) continue;
-#pragma unroll
-                for (int ni = 0; ni < FT; ++ni) {
-                    const int n = n0 + wn * WT + ni * 16 + (lane & 15);
-                    if (n < g.N) ((float*)g.C)[(m / g.c_grp_rows) * g.c_grp_stride + (int64_t)(m % g.c_grp_rows) * g.ldc + n] =
-                        g.bias ? acc[mi][ni][i] + g.bias[n] : acc[mi][ni][i];
-                }
-            }
-    }
-}
-
-template <int EPI>
-void launch_pipe128(const GemmArgs& g, hipStream_t s) {
-    set_lds_once((const void*)gemm128_pipe_kernel<EPI>, R128_LDS);
-    const int nwg = ((g.N + 127) / 128) * ((g.M + 127) / 128);
-    gemm128_pipe_kernel<EPI><<<nwg, NTHR, R128_LDS, s>>>(g);
-}
-
 template <int EPI>
 void launch_ring128(const GemmArgs& g, hipStream_t s) {
     set_lds_once((const void*)gemm128_ring_kernel<EPI>, R128_LDS);
@@ -1437,7 +1284,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL ? 4 : 1
     // (48 hi/lo rows: 128-deep chunks, so the 4 waves' 1-KiB staging pieces cover all 48
     // rows; a 64-deep chunk stages 32 rows per round and would leave rows 32-47 unstaged.
     // Not reachable from the launchers, which group hi/lo rows by 32; kept valid anyway.)
-    constexpr int CK = (LO && MT >= 2) ? (MT == 3 ? 4 : 2) : 8;
+    // 16-row hi/lo groups (2..16 decoder rows: beam 5 of one to three windows, greedy
+    // batches) stream 128-deep chunks: 16 KiB of LDS, so the workgroup fits beside another
+    // lane's 128-KiB encoder workgroup (<= 30 KiB free) instead of waiting for its tile to
+    // retire; the fused batch-1 forms (PRO) keep 256-deep chunks
+    constexpr int CK = (LO && MT >= 2) ? (MT == 3 ? 4 : 2) : (LO && PRO == PRO_NONE) ? OSW_SKINNY_CK1 : 8;
     constexpr int CKK = CK * 32;                 // k per chunk
     constexpr int CPR = CKK / 8;                 // 16-B pieces of one row per chunk
     constexpr int RPP = 64 / CPR;                // rows per 1-KiB glds wave-instruction
@@ -2057,7 +1908,6 @@ void prepare_gemm_kernels() {
             set_lds_once((const void*)gemm256_kernel<E>, l256);
             set_lds_once((const void*)gemm8p_kernel<E, 0>, l8p);
             set_lds_once((const void*)gemm128_ring_kernel<E>, R128_LDS);
-            set_lds_once((const void*)gemm128_pipe_kernel<E>, R128_LDS);
         };
         each(std::integral_constant<int, EPI_F16>{});
         each(std::integral_constant<int, EPI_F16_GELU>{});
@@ -2112,16 +1962,6 @@ void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s) {
     if (variant == 10) {
         launch8p<EPI_F16_GELU>(g, s);
         return;
-    }
-    if (variant == 14) {  // the software-pipelined 128 tile (gemm128_pipe_kernel)
-        switch (g.epi) {
-            case EPI_F16: launch_pipe128<EPI_F16>(g, s); return;
-            case EPI_F16_GELU: launch_pipe128<EPI_F16_GELU>(g, s); return;
-            case EPI_F32_RESID: launch_pipe128<EPI_F32_RESID>(g, s); return;
-            case EPI_F32_GELU_POS: launch_pipe128<EPI_F32_GELU_POS>(g, s); return;
-            case EPI_F32: launch_pipe128<EPI_F32>(g, s); return;
-            default: launch_pipe128<EPI_HEADS>(g, s); return;
-        }
     }
     if (variant == 12 || variant == 13) {  // debug: fp16 / GELU epilogues on accumulators not transposed
         if (variant == 12) launch8p<EPI_F16, 2>(g, s);

@@ -193,6 +193,43 @@ int osw_transcribe_refill(osw_ctx* ctx, const int16_t* pcm, const int64_t* offse
                           int32_t pcm_on_device, const osw_decode_opts* opts, osw_window_result* res,
                           int32_t refill_min);
 
+/* ---- decode sessions: continuous batching of windows (greedy or beam search) ----
+ * A session keeps max_batch window slots on the context (beam search: beam_size decoder
+ * rows per slot, each with its own step counter and prompt).  Windows are queued with
+ * osw_session_add and admitted into free slots between chunks of 8 decoder steps (their
+ * encoder runs straight into the slot's cross-K/V); a finished window leaves its slot at
+ * once.  So a window queued while others decode joins at the next chunk instead of
+ * waiting for the longest window of a batch, and a caller can queue the next window of a
+ * file (its previous-text prefix included) as soon as the previous one finished.  Each
+ * window's result equals osw_decode_windows's for it alone: rows are independent in every
+ * kernel.  Replaces the per-request WhisperModel.transcribe loops that the reference runs
+ * from concurrent executor threads (src/main.py:305, src/streaming.py:366-375,
+ * src/backends/faster_whisper.py:235-246) with one decoder batch per context.
+ * opts: temperature 0 (greedy, or beam search with beam_size <= 5); its prefix_tokens,
+ * language_tokens and token_budget are ignored (per window below).  While a session is
+ * open the context's other decode entry points return OSW_EINVAL. */
+typedef struct osw_session_window {
+    int64_t tag;              /* the caller's id, returned with the result */
+    int32_t seek;             /* first mel frame of the window in its clip */
+    int32_t segment_size;     /* frames (<= 3000) */
+    int32_t language_token;   /* -1: detect */
+    int32_t token_budget;     /* length control (benches): <= 0 none */
+    int32_t n_prefix;         /* previous-text prompt tokens before <|startoftranscript|> */
+    const int32_t* prefix;    /* <|startofprev|> and the previous tokens, or NULL */
+} osw_session_window;
+int osw_session_begin(osw_ctx* ctx, const osw_decode_opts* opts);
+/* Queue n windows; window i reads clip pcm[offsets[i], offsets[i+1]) (host int16, copied). */
+int osw_session_add(osw_ctx* ctx, const int16_t* pcm, const int64_t* offsets, int32_t n,
+                    const osw_session_window* windows);
+/* Admit queued windows into free slots (when at least min(refill_min, queued) slots are
+ * free, or nothing decodes) and run up to max_chunks chunks of decoder steps, returning
+ * after the first chunk in which windows finished.  Their results go to res[0 .. *n_done)
+ * (res->tokens rows of res->max_tokens), their tags to tags_out; cap >= max_batch.
+ * *n_active / *n_queued: windows decoding / waiting after the call. */
+int osw_session_step(osw_ctx* ctx, int32_t max_chunks, int32_t refill_min, osw_window_result* res,
+                     int64_t* tags_out, int32_t cap, int32_t* n_done, int32_t* n_active, int32_t* n_queued);
+int osw_session_end(osw_ctx* ctx);
+
 /* Parity helper: one encoder block on x [T][D] fp32 (host), result to y (host). */
 int osw_encoder_layer_debug(osw_ctx* ctx, int32_t layer, const float* x, float* y, int32_t T);
 

@@ -9,13 +9,18 @@ namespace osw {
 struct SelState {
     int n_sampled, last, penult, last_ts, done, lang;
     float sum_lp, nsp;  // greedy: Σ log-prob of the picks; beam: the hypothesis' cumulative score
+    int plen;           // this row's prompt length (0: SelParams::prompt_len; decode sessions admit
+                        // windows with different previous-text prefixes)
+    int pad;
 };
 
 struct SelParams {
-    int prompt_len;        // P: positions 0..P-1 are prompt
+    int prompt_len;        // P: positions 0..P-1 are prompt (rows whose SelState::plen is 0)
     int sot_pos;           // position of <|startoftranscript|> in the prompt
     int lang_pos;          // prompt position holding the language token (-1 placeholder => detect)
     int max_length;
+    int pstride;           // ints per row of the prompt buffer (>= every row's prompt length)
+    int tail;              // prompt positions from <|startoftranscript|> to the end (3, or 4 with no-timestamps)
     int V, eot, no_speech, no_ts, tb, blank, first_lang, n_langs;
     int suppress_blank, with_ts, max_init_ts;
     int beam;              // hypotheses per window (1 = greedy)
@@ -26,8 +31,13 @@ struct SelParams {
                                      // seed per call replays the captured decode graph)
     const int* budget;     // per decoder row: force <|endoftext|> after this many sampled tokens (<= 0: none);
                            // nullptr: no budgets (osw_decode_opts::token_budget, length-controlled benches)
-    int pos_row;           // 1: row r's step counter is pos[r] (row refill, greedy), 0: one shared counter
+    int pos_row;           // 1: row r's step counter is pos[r] (row refill, sessions), 0: one shared counter
 };
+
+// the row's prompt length and <|startoftranscript|> position
+__host__ __device__ __forceinline__ int row_plen(const SelParams& P, const SelState& s) {
+    return s.plen > 0 ? s.plen : P.prompt_len;
+}
 
 // Per window in beam mode: finished-hypothesis bookkeeping (the best one's tokens
 // are copied to a per-window buffer when it improves).
@@ -59,6 +69,8 @@ constexpr int XPART = 72;     // floats per (decoder row, head, key chunk) cross
 constexpr int XCHUNKS = 8;    // fixed key chunks per (window, head) in cross-attention
 constexpr int SEL_SPLIT = 16;  // vocabulary slices per row in the selection kernels
 
+void launch_session_rows(const int* pack, int k, int ps, int group, int pstride, int ctx, int* prompt, int* budget,
+                         int* cur_tok, int* pos, SelState* st, int* anc, BeamWin* bwin, hipStream_t s);
 void launch_refill_rows(const int* pack, int k, int P, int* prompt, int* budget, int* cur_tok, int* pos, SelState* st,
                         hipStream_t s);
 void launch_select(const float* logits, int rows, int* pos, const SelParams& P, const int* prompt,

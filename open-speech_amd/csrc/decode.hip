@@ -1009,7 +1009,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void s
         if (sel_mode(P, step, s) == SEL_SAMPLE) {  // the same for every slice of the row
             // beam rows' sampling steps: statistics + candidates in one pass; nothing to
             // finalise here (beam_update picks), so no ticket
-            if (step == P.prompt_len - 1 && blockIdx.x % P.beam != 0) return;  // only the prompt hypothesis expands
+            if (step == row_plen(P, s) - 1 && blockIdx.x % P.beam != 0) return;  // only the prompt hypothesis expands
             beam_slice_body<MODE == 2>(logits, P, step, supmask, s, parts, cand);
             return;
         }
@@ -1090,7 +1090,7 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
     __shared__ int choose[KM], fin, best_src, best_extra, improved;
     const int w = blockIdx.x, tid = threadIdx.x, K = P.beam, K2 = 2 * K;
     const int r0 = w * K;
-    const int step = *pos_ptr;
+    const int step = pos_ptr[P.pos_row ? r0 : 0];
     if (sel_mode(P, step, st[r0]) != SEL_SAMPLE) return;
     const int nc = K * BEAM_SLICES * K2;
     const int n = st[r0].n_sampled;  // identical for every row of the window
@@ -1113,7 +1113,8 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
     __syncthreads();
     // candidate (row k, slice, j): list B if the row's timestamps win, else list A; score =
     // sum_lp + (x - lse) as the per-row log-prob + cumulative score of the reference
-    const bool first = step == P.prompt_len - 1;  // only the prompt hypothesis expands
+    const int plen = row_plen(P, st[r0]);
+    const bool first = step == plen - 1;  // only the prompt hypothesis expands
     for (int i0 = tid; i0 < nc; i0 += 256 * LB) {
         BeamCand c[LB];
 #pragma unroll
@@ -1178,7 +1179,7 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
     if (tid == 0) {
         BeamWin bw = bwin[w];
         // the last step: max_length, or (length control) the window's token budget
-        const bool is_last = P.prompt_len + n + 1 >= P.max_length || (P.budget && P.budget[r0] > 0 && n + 1 >= P.budget[r0]);
+        const bool is_last = plen + n + 1 >= P.max_length || (P.budget && P.budget[r0] > 0 && n + 1 >= P.budget[r0]);
         int sec = K;
         bool top_fin = false;
         improved = 0;
@@ -1262,9 +1263,13 @@ __global__ __launch_bounds__(256) void beam_update_kernel(SelParams P, int* __re
                                                           int* __restrict__ anc, int ctx, BeamWin* __restrict__ bwin,
                                                           int* __restrict__ best_tok, int* __restrict__ cur_tok,
                                                           int max_tokens, int* __restrict__ arrive) {
-    const int step = *pos_ptr;
+    const int step = pos_ptr[P.pos_row ? blockIdx.x * P.beam : 0];
     beam_update_body<KM>(P, pos_ptr, st, parts, cand, seq, anc, ctx, bwin, best_tok, cur_tok, max_tokens);
     __syncthreads();
+    if (P.pos_row) {  // a session: this window's rows advance their own counters
+        if (threadIdx.x < P.beam) pos_ptr[blockIdx.x * P.beam + threadIdx.x] = step + 1;
+        return;
+    }
     if (threadIdx.x != 0) return;
     __builtin_amdgcn_s_waitcnt(0);
     if (__hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
@@ -1286,6 +1291,32 @@ __global__ __launch_bounds__(64) void refill_rows_kernel(const int* __restrict__
         cur_tok[row] = e[2];
         pos[row] = 0;
         st[row] = SelState{};
+    }
+}
+
+// Decode sessions (osw.hip, osw_session_*): reset the `group` rows of each admitted window
+// slot.  pack[i] = {slot, plen, budget, prompt[0 .. plen)} with stride `ps`; grid (windows,
+// group), 64 threads.  Beam rows (anc != nullptr) also get an identity ancestry and the
+// window's hypothesis bookkeeping a fresh start.
+__global__ __launch_bounds__(64) void session_rows_kernel(const int* __restrict__ pack, int ps, int group,
+                                                          int pstride, int ctx, int* __restrict__ prompt,
+                                                          int* __restrict__ budget, int* __restrict__ cur_tok,
+                                                          int* __restrict__ pos, SelState* __restrict__ st,
+                                                          int* __restrict__ anc, BeamWin* __restrict__ bwin) {
+    const int* e = pack + (int64_t)blockIdx.x * ps;
+    const int slot = e[0], plen = e[1];
+    const int row = slot * group + blockIdx.y;
+    for (int j = threadIdx.x; j < plen; j += blockDim.x) prompt[(int64_t)row * pstride + j] = e[3 + j];
+    if (anc)
+        for (int p = threadIdx.x; p < ctx; p += blockDim.x) anc[(int64_t)row * ctx + p] = row;
+    if (threadIdx.x == 0) {
+        budget[row] = e[2];
+        cur_tok[row] = e[3];
+        pos[row] = 0;
+        SelState s{};
+        s.plen = plen;
+        st[row] = s;
+        if (bwin && blockIdx.y == 0) bwin[slot] = BeamWin{};
     }
 }
 
@@ -1417,6 +1448,12 @@ void launch_beam(const float* logits, int windows, int* pos, const SelParams& P,
         beam_update_kernel<MAX_BEAM><<<windows, 256, 0, s>>>(P, pos, st, (const SelPart*)sel_parts,
                                                              (const BeamCand*)cand, seq, anc, ctx, bw, best_tok, cur_tok,
                                                              max_tokens, arrive);
+}
+
+void launch_session_rows(const int* pack, int k, int ps, int group, int pstride, int ctx, int* prompt, int* budget,
+                         int* cur_tok, int* pos, SelState* st, int* anc, BeamWin* bwin, hipStream_t s) {
+    session_rows_kernel<<<dim3(k, group), 64, 0, s>>>(pack, ps, group, pstride, ctx, prompt, budget, cur_tok, pos, st,
+                                                      anc, bwin);
 }
 
 void launch_count_done(const SelState* st, int rows, int* out, hipStream_t s) {

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <pthread.h>
 #include <functional>
@@ -209,7 +210,10 @@ struct osw_ctx {
         *XKV = nullptr;
     float* X = nullptr;
     int n_encoded = 0;
-    bool row_pos = false;             // decode_refill: per-row step counters (pos[row])
+    bool row_pos = false;             // decode_refill / sessions: per-row step counters (pos[row])
+    int kv_rows = 0;                  // sessions: self-K/V cache rows per layer (0: the step's row count)
+    int xkv_windows = 0;              // sessions: cross-K/V windows per layer (0: the step's windows)
+    struct Session* sess = nullptr;   // an open decode session (osw_session_*)
     int* slot_d = nullptr;            // encode into slots: window -> decoder row
     int* refill_pack = nullptr;       // decode_refill: rows to admit {row, budget, prompt}
 
@@ -545,7 +549,7 @@ void setup_workspace(osw_ctx* c) {
     c->cur_tok = dalloc<int>(R, o);
     c->pos = dalloc<int>(R, o);  // [0]: the shared step counter; [row] in decode_refill
     c->slot_d = dalloc<int>(B, o);
-    c->refill_pack = dalloc<int>(B * (2 + d.n_text_ctx), o);
+    c->refill_pack = dalloc<int>(B * (3 + d.n_text_ctx), o);  // (sessions: {slot, plen, budget, prompt})
     c->tokens = dalloc<int>(R * d.n_text_ctx, o);
     c->prompt = dalloc<int>(R * d.n_text_ctx, o);
     c->done = dalloc<int>(1, o);
@@ -765,8 +769,8 @@ void encode(osw_ctx* c, const osw_window* wins, int n, const int* slots = nullpt
 void decoder_step_fused(osw_ctx* c, int nb, int group, bool gather, const SelFuse* sf) {
     const osw_dims& d = c->d;
     const int D = d.n_text_state, H = d.n_text_head, L = d.n_text_layer, ctx = d.n_text_ctx;
-    const int64_t xkv_which = (int64_t)(nb / group) * H * T_ENC * 64;
-    const int64_t kv_layer = (int64_t)nb * H * ctx * 64;
+    const int64_t xkv_which = (int64_t)(c->xkv_windows ? c->xkv_windows : nb / group) * H * T_ENC * 64;
+    const int64_t kv_layer = (int64_t)(c->kv_rows ? c->kv_rows : nb) * H * ctx * 64;
     const int64_t lo_d = (int64_t)c->R * D;
     float* xs[2] = {c->xd, c->xd2};
     float* ps[2] = {c->part, c->part2};
@@ -836,8 +840,8 @@ void decoder_step_fused(osw_ctx* c, int nb, int group, bool gather, const SelFus
 bool decoder_step(osw_ctx* c, int nb, int group, bool gather, const SelFuse* sf = nullptr) {
     const osw_dims& d = c->d;
     const int D = d.n_text_state, H = d.n_text_head, L = d.n_text_layer, ctx = d.n_text_ctx;
-    const int64_t xkv_which = (int64_t)(nb / group) * H * T_ENC * 64;
-    const int64_t kv_layer = (int64_t)nb * H * ctx * 64;
+    const int64_t xkv_which = (int64_t)(c->xkv_windows ? c->xkv_windows : nb / group) * H * T_ENC * 64;
+    const int64_t kv_layer = (int64_t)(c->kv_rows ? c->kv_rows : nb) * H * ctx * 64;
     REQUIRE(nb <= c->R && D <= 1280, "decoder step: rows <= capacity and D <= 1280");
     REQUIRE(ctx <= 448, "decoder self-attention holds at most 448 positions");
     // the decoder's GEMM operands are hi/lo fp16 pairs (fp32-accurate activations: the
@@ -1029,6 +1033,7 @@ void decode(osw_ctx* c, int nb, const osw_decode_opts* o, osw_window_result* r) 
     }
     SelParams SP{};
     SP.prompt_len = P; SP.sot_pos = n_pre; SP.lang_pos = n_pre + 1; SP.max_length = max_len;
+    SP.pstride = P; SP.tail = P - n_pre;
     SP.V = V; SP.eot = o->eot; SP.no_speech = o->no_speech; SP.no_ts = o->no_timestamps; SP.tb = o->timestamp_begin;
     SP.blank = o->blank; SP.first_lang = o->first_lang; SP.n_langs = o->n_langs;
     SP.suppress_blank = o->suppress_blank; SP.with_ts = o->without_timestamps ? 0 : 1;
@@ -1177,6 +1182,7 @@ void decode_refill(osw_ctx* c, int n_clips, const osw_decode_opts* o, osw_window
     }
     SelParams SP{};
     SP.prompt_len = P; SP.sot_pos = 0; SP.lang_pos = 1; SP.max_length = max_len;
+    SP.pstride = P; SP.tail = P;
     SP.V = V; SP.eot = o->eot; SP.no_speech = o->no_speech; SP.no_ts = o->no_timestamps; SP.tb = o->timestamp_begin;
     SP.blank = o->blank; SP.first_lang = o->first_lang; SP.n_langs = o->n_langs;
     SP.suppress_blank = o->suppress_blank; SP.with_ts = o->without_timestamps ? 0 : 1;
@@ -1450,6 +1456,243 @@ int64_t upfirdn_output_len(int64_t len_h, int64_t n_in, int64_t up, int64_t down
 
 }  // namespace
 
+// ------------------------------ decode sessions ------------------------------
+// Continuous batching (osw_session_*, include/osw.h): c->B window slots, `beam` decoder rows
+// each (rows slot*beam .. slot*beam+beam-1), per-row step counters (pos[row]), per-row prompts
+// (SelState::plen, prompt rows of n_text_ctx ints).  The self-K/V cache and the cross-K/V
+// keep their full-capacity layouts (ctx->kv_rows, ctx->xkv_windows), so a step may cover only
+// the rows up to the highest occupied slot.  Windows are admitted between chunks of CH steps:
+// their log-mel, their encoder straight into the slots' cross-K/V, then the rows' reset.
+struct SessionWin {
+    std::vector<int16_t> pcm;
+    std::vector<int> prefix;
+    osw_session_window w;
+};
+struct Session {
+    osw_decode_opts o{};
+    SelParams SP{};
+    int beam = 1, W = 0, tail = 3, max_len = 448, max_tok = 445, ctx = 448;
+    std::vector<int64_t> slot_tag;
+    std::deque<SessionWin> queue;
+    int active = 0;
+    int64_t steps = 0;
+};
+
+namespace {
+using osw::SelState;
+
+void session_begin(osw_ctx* c, const osw_decode_opts* o) {
+    REQUIRE(o, "null decode options");
+    REQUIRE(!c->sess, "a decode session is already open on this context");
+    REQUIRE(!(o->temperature > 0.f), "decode sessions decode at temperature 0 (greedy or beam search)");
+    const osw_dims& d = c->d;
+    const int V = d.n_vocab;
+    REQUIRE(V <= SEL_SPLIT * 4096, "vocabulary too large for the selection kernels");
+    auto S = std::make_unique<Session>();
+    S->o = *o;
+    S->beam = std::max(1, o->beam_size);
+    REQUIRE(S->beam <= 5, "decode sessions hold beam_size <= 5 (5 decoder rows per window slot)");
+    S->W = c->B;
+    S->ctx = d.n_text_ctx;
+    S->tail = 3 + (o->without_timestamps ? 1 : 0);
+    S->max_len = std::min(o->max_length > 0 ? o->max_length : d.n_text_ctx, d.n_text_ctx);
+    REQUIRE(S->tail < S->max_len, "prompt longer than max_length");
+    S->max_tok = std::max(1, S->max_len - S->tail);
+    std::vector<unsigned> mask((V + 31) / 32, 0u);
+    for (int i = 0; i < o->n_suppress; ++i) {
+        const int t = o->suppress_tokens[i];
+        if (t >= 0 && t < V) mask[t >> 5] |= 1u << (t & 31);
+    }
+    SelParams& SP = S->SP;
+    SP.prompt_len = S->tail; SP.sot_pos = 0; SP.lang_pos = 1; SP.max_length = S->max_len;
+    SP.pstride = S->ctx; SP.tail = S->tail;
+    SP.V = V; SP.eot = o->eot; SP.no_speech = o->no_speech; SP.no_ts = o->no_timestamps; SP.tb = o->timestamp_begin;
+    SP.blank = o->blank; SP.first_lang = o->first_lang; SP.n_langs = o->n_langs;
+    SP.suppress_blank = o->suppress_blank; SP.with_ts = o->without_timestamps ? 0 : 1;
+    SP.max_init_ts = o->max_initial_timestamp_index;
+    SP.beam = S->beam;
+    SP.num_hyp = std::max(1, o->num_hypotheses);
+    SP.max_cand = std::max(1, (int)std::lround(S->beam * (o->patience > 0.f ? o->patience : 1.f)));
+    SP.length_penalty = o->length_penalty;
+    SP.inv_temp = 0.f;
+    HIPCHK(hipMemcpyAsync(c->seed_d, &o->seed, 8, hipMemcpyHostToDevice, c->stream));
+    SP.seed = c->seed_d;
+    SP.budget = c->budget;
+    SP.pos_row = 1;
+    S->o.suppress_tokens = nullptr;  // (copied into the mask)
+    S->o.prefix_tokens = nullptr;
+    S->o.language_tokens = nullptr;
+    S->o.token_budget = nullptr;
+    const int R = S->W * S->beam;
+    std::vector<SelState> st(R);
+    for (auto& q : st) q = SelState{}, q.done = 1;
+    HIPCHK(hipMemcpyAsync(c->supmask, mask.data(), mask.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->sel, st.data(), (size_t)R * sizeof(SelState), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemsetAsync(c->pos, 0, (size_t)R * 4, c->stream));
+    HIPCHK(hipMemsetAsync(c->cur_tok, 0, (size_t)R * 4, c->stream));
+    HIPCHK(hipMemsetAsync(c->budget, 0, (size_t)R * 4, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    S->slot_tag.assign(S->W, -1);
+    c->row_pos = true;
+    c->kv_rows = c->R;
+    c->xkv_windows = c->B;
+    c->sess = S.release();
+}
+
+void session_end(osw_ctx* c) {
+    delete c->sess;
+    c->sess = nullptr;
+    c->row_pos = false;
+    c->kv_rows = 0;
+    c->xkv_windows = 0;
+    c->n_encoded = 0;
+}
+
+void session_add(osw_ctx* c, const int16_t* pcm, const int64_t* offsets, int n, const osw_session_window* w) {
+    Session* S = c->sess;
+    REQUIRE(S, "no decode session open");
+    REQUIRE(pcm && offsets && w && n >= 0, "null argument");
+    for (int i = 0; i < n; ++i) {
+        REQUIRE(offsets[i + 1] >= offsets[i], "offsets must not decrease");
+        REQUIRE(w[i].segment_size >= 1 && w[i].seek >= 0, "empty window");
+        REQUIRE(w[i].n_prefix >= 0 && (w[i].n_prefix == 0 || w[i].prefix), "bad prefix");
+        REQUIRE(w[i].n_prefix + S->tail < S->max_len, "prompt longer than max_length");
+        // (log_mel's frame count: one frame per 160 samples, plus one)
+        REQUIRE(w[i].seek < (int)((offsets[i + 1] - offsets[i] + 160) / 160), "window seek out of range");
+        SessionWin q;
+        q.pcm.assign(pcm + offsets[i], pcm + offsets[i + 1]);
+        q.prefix.assign(w[i].prefix, w[i].prefix + w[i].n_prefix);
+        q.w = w[i];
+        q.w.prefix = nullptr;
+        S->queue.push_back(std::move(q));
+    }
+}
+
+void session_admit(osw_ctx* c, int refill_min) {
+    Session* S = c->sess;
+    std::vector<int> free_slots;
+    for (int i = 0; i < S->W; ++i)
+        if (S->slot_tag[i] < 0) free_slots.push_back(i);
+    const int queued = (int)S->queue.size();
+    if (!queued || free_slots.empty()) return;
+    if (S->active > 0 && (int)free_slots.size() < std::min(std::max(1, refill_min), queued)) return;
+    const int k = std::min((int)free_slots.size(), queued);
+    std::vector<int16_t> pcm;
+    std::vector<int64_t> offs(k + 1, 0);
+    for (int i = 0; i < k; ++i) {
+        pcm.insert(pcm.end(), S->queue[i].pcm.begin(), S->queue[i].pcm.end());
+        offs[i + 1] = (int64_t)pcm.size();
+    }
+    if (pcm.empty()) pcm.push_back(0);
+    log_mel(c, pcm.data(), offs.data(), k, 0, nullptr);
+    const int ps = 3 + S->ctx;
+    std::vector<osw_window> wins(k);
+    std::vector<int> slots(k), pack((size_t)k * ps, 0);
+    for (int i = 0; i < k; ++i) {
+        const SessionWin& q = S->queue[i];
+        const int slot = free_slots[i];
+        wins[i] = osw_window{i, q.w.seek, q.w.segment_size};
+        slots[i] = slot;
+        int* e = &pack[(size_t)i * ps];
+        const int np = (int)q.prefix.size();
+        e[0] = slot;
+        e[1] = np + S->tail;
+        e[2] = q.w.token_budget;
+        for (int j = 0; j < np; ++j) e[3 + j] = q.prefix[j];
+        e[3 + np] = S->o.sot;
+        e[3 + np + 1] = q.w.language_token;  // -1: detect
+        e[3 + np + 2] = S->o.task_token;
+        if (S->o.without_timestamps) e[3 + np + 3] = S->o.no_timestamps;
+    }
+    encode(c, wins.data(), k, slots.data());
+    for (int i = 0; i < k; ++i) S->slot_tag[free_slots[i]] = S->queue[i].w.tag;
+    HIPCHK(hipMemcpyAsync(c->refill_pack, pack.data(), pack.size() * 4, hipMemcpyHostToDevice, c->stream));
+    launch_session_rows(c->refill_pack, k, ps, S->beam, S->ctx, S->ctx, c->prompt, c->budget, c->cur_tok, c->pos,
+                        c->sel, S->beam > 1 ? c->anc : nullptr, S->beam > 1 ? c->bwin : nullptr, c->stream);
+    HIPCHK(hipGetLastError());
+    for (int i = 0; i < k; ++i) S->queue.pop_front();
+    S->active += k;
+}
+
+// returns the number of finished windows written to r / tags
+int session_step(osw_ctx* c, int max_chunks, int refill_min, osw_window_result* r, int64_t* tags, int cap) {
+    Session* S = c->sess;
+    REQUIRE(S, "no decode session open");
+    REQUIRE(r && r->tokens && r->n_tokens && r->sum_logprob && r->no_speech_prob && r->language && tags,
+            "null result argument");
+    REQUIRE(cap >= S->W, "cap must hold every slot (max_batch)");
+    const int beam = S->beam, CH = 8;
+    int done = 0;
+    for (int chunk = 0; chunk < max_chunks && done == 0; ++chunk) {
+        session_admit(c, refill_min);
+        if (S->active == 0) break;
+        int hi = 0;
+        for (int i = 0; i < S->W; ++i)
+            if (S->slot_tag[i] >= 0) hi = i + 1;
+        hi = std::min(S->W, (hi + 3) / 4 * 4);  // (fewer graph shapes; idle slots' rows are finished)
+        const int nb = hi * beam;
+        const SelParams& SP = S->SP;
+        auto one_step = [&] {
+            decoder_step(c, nb, beam, beam > 1, nullptr);
+            launch_select(c->logits, nb, c->pos, SP, c->prompt, c->supmask, c->sel, c->cur_tok, c->tokens, S->max_tok,
+                          c->selp, c->sel_arrive, beam == 1, c->bcand, c->stream);
+            if (beam > 1)
+                launch_beam(c->logits, hi, c->pos, SP, c->supmask, c->sel, c->selp, c->bcand, c->tokens, c->anc, S->ctx,
+                            c->bwin, c->btok, c->cur_tok, S->max_tok, c->sel_arrive, c->stream);
+        };
+        if (c->use_graph && !c->prof_eager) {
+            int32_t lp_bits;
+            std::memcpy(&lp_bits, &SP.length_penalty, 4);
+            // (the -2 tail keeps session keys apart from decode()'s and the refill's)
+            const std::vector<int64_t> key = {nb, S->tail, 0, S->max_len, S->o.eot, S->o.no_speech, S->o.no_timestamps,
+                                              S->o.timestamp_begin, S->o.blank, S->o.first_lang, S->o.n_langs,
+                                              S->o.suppress_blank, S->o.without_timestamps,
+                                              S->o.max_initial_timestamp_index, beam, SP.num_hyp, SP.max_cand, lp_bits,
+                                              beam, 0, 1, -2};
+            hipGraphExec_t ge = decode_graph(c, key, one_step, CH);
+            trace_graph(c, "launch");
+            HIPCHK(hipGraphLaunch(ge, c->stream));
+        } else {
+            for (int i = 0; i < CH; ++i) one_step();
+        }
+        HIPCHK(hipGetLastError());
+        S->steps += CH;
+        std::vector<SelState> st(nb);
+        std::vector<BeamWin> bw(beam > 1 ? hi : 0);
+        HIPCHK(hipMemcpyAsync(st.data(), c->sel, (size_t)nb * sizeof(SelState), hipMemcpyDeviceToHost, c->stream));
+        if (beam > 1)
+            HIPCHK(hipMemcpyAsync(bw.data(), c->bwin, (size_t)hi * sizeof(BeamWin), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        std::vector<int> fin;
+        for (int i = 0; i < hi; ++i)
+            if (S->slot_tag[i] >= 0 && (beam > 1 ? bw[i].done : st[i].done)) fin.push_back(i);
+        if (fin.empty()) continue;
+        // the finished windows' tokens: beam -> the best hypothesis per window (btok),
+        // greedy -> the row's picks (tokens)
+        std::vector<int> toks((size_t)hi * S->max_tok);
+        HIPCHK(hipMemcpyAsync(toks.data(), beam > 1 ? c->btok : c->tokens, toks.size() * 4, hipMemcpyDeviceToHost,
+                              c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        for (int slot : fin) {
+            const SelState& q = st[(size_t)slot * beam];
+            const int n0 = beam > 1 ? bw[slot].best_len : q.n_sampled;
+            const int n = std::min(n0, std::min(S->max_tok, r->max_tokens));
+            r->n_tokens[done] = n;
+            for (int j = 0; j < n; ++j) r->tokens[(size_t)done * r->max_tokens + j] = toks[(size_t)slot * S->max_tok + j];
+            r->sum_logprob[done] = beam > 1 ? bw[slot].best_raw : q.sum_lp;
+            r->no_speech_prob[done] = q.nsp;
+            r->language[done] = q.lang;
+            tags[done] = S->slot_tag[slot];
+            S->slot_tag[slot] = -1;
+            --S->active;
+            ++done;
+        }
+    }
+    c->pf.decode_steps = S->steps;
+    return done;
+}
+}  // namespace
+
 // ============================== C ABI =======================================
 extern "C" {
 
@@ -1578,6 +1821,8 @@ int osw_destroy(osw_ctx* c) {
             for (auto& e : c->evs) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
             for (auto e : c->ev_free) (void)hipEventDestroy(e);
             for (auto& kv : c->dgraphs) (void)hipGraphExecDestroy(kv.second.first);
+            delete c->sess;
+            c->sess = nullptr;
             for (void* p : c->owned) (void)hipFree(p);
             if (c->done_host) (void)hipHostFree(c->done_host);
             destroy_streams(c);
@@ -1692,6 +1937,7 @@ int osw_encode_windows(osw_ctx* c, const osw_window* windows, int32_t n) {
     return guard([&] {
         REQUIRE(c && windows, "null argument");
         std::lock_guard<std::mutex> lk(c->mu);
+        REQUIRE(!c->sess, "a decode session is open on this context (osw_session_end first)");
         DeviceScope dev_scope_((c->device));
         LaneCall call_(c);
         encode(c, windows, n);
@@ -1718,6 +1964,7 @@ int osw_decode_windows(osw_ctx* c, int32_t n, const osw_decode_opts* opts, osw_w
     return guard([&] {
         REQUIRE(c, "null ctx");
         std::lock_guard<std::mutex> lk(c->mu);
+        REQUIRE(!c->sess, "a decode session is open on this context (osw_session_end first)");
         DeviceScope dev_scope_((c->device));
         LaneCall call_(c);
         decode(c, n, opts, res);
@@ -1730,6 +1977,7 @@ int osw_transcribe_batch(osw_ctx* c, const int16_t* pcm, const int64_t* offsets,
     return guard([&] {
         REQUIRE(c, "null ctx");
         std::lock_guard<std::mutex> lk(c->mu);
+        REQUIRE(!c->sess, "a decode session is open on this context (osw_session_end first)");
         DeviceScope dev_scope_((c->device));
         REQUIRE(n_clips >= 1 && n_clips <= c->B, "n_clips out of range");
         LaneCall call_(c);
@@ -1749,12 +1997,55 @@ int osw_transcribe_refill(osw_ctx* c, const int16_t* pcm, const int64_t* offsets
     return guard([&] {
         REQUIRE(c, "null ctx");
         std::lock_guard<std::mutex> lk(c->mu);
+        REQUIRE(!c->sess, "a decode session is open on this context (osw_session_end first)");
         DeviceScope dev_scope_((c->device));
         REQUIRE(n_clips >= 1, "n_clips out of range");
         LaneCall call_(c);
         log_mel(c, pcm, offsets, n_clips, pcm_on_device, nullptr);
         decode_refill(c, n_clips, opts, res, refill_min);
         resolve_events(c);
+    });
+}
+
+int osw_session_begin(osw_ctx* c, const osw_decode_opts* opts) {
+    return guard([&] {
+        REQUIRE(c, "null ctx");
+        std::lock_guard<std::mutex> lk(c->mu);
+        DeviceScope dev_scope_((c->device));
+        session_begin(c, opts);
+    });
+}
+
+int osw_session_add(osw_ctx* c, const int16_t* pcm, const int64_t* offsets, int32_t n,
+                    const osw_session_window* windows) {
+    return guard([&] {
+        REQUIRE(c, "null ctx");
+        std::lock_guard<std::mutex> lk(c->mu);
+        session_add(c, pcm, offsets, n, windows);
+    });
+}
+
+int osw_session_step(osw_ctx* c, int32_t max_chunks, int32_t refill_min, osw_window_result* res, int64_t* tags_out,
+                     int32_t cap, int32_t* n_done, int32_t* n_active, int32_t* n_queued) {
+    return guard([&] {
+        REQUIRE(c && n_done && n_active && n_queued, "null argument");
+        std::lock_guard<std::mutex> lk(c->mu);
+        DeviceScope dev_scope_((c->device));
+        LaneCall call_(c);
+        *n_done = session_step(c, std::max(1, max_chunks), refill_min, res, tags_out, cap);
+        *n_active = c->sess->active;
+        *n_queued = (int32_t)c->sess->queue.size();
+        resolve_events(c);
+    });
+}
+
+int osw_session_end(osw_ctx* c) {
+    return guard([&] {
+        REQUIRE(c, "null ctx");
+        std::lock_guard<std::mutex> lk(c->mu);
+        DeviceScope dev_scope_((c->device));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        session_end(c);
     });
 }
 

@@ -46,7 +46,11 @@ struct SelPart {
 enum { SEL_PROMPT = 0, SEL_SOT = 1, SEL_SAMPLE = 2, SEL_DONE = 3 };
 
 __device__ __forceinline__ int sel_mode(const SelParams& P, int step, const SelState& s) {
-    if (step < P.prompt_len - 1) return step == P.sot_pos ? SEL_SOT : SEL_PROMPT;
+    if (s.plen > 0) {  // a session row: its own prompt length
+        if (step < s.plen - 1) return step == s.plen - P.tail ? SEL_SOT : SEL_PROMPT;
+    } else if (step < P.prompt_len - 1) {
+        return step == P.sot_pos ? SEL_SOT : SEL_PROMPT;
+    }
     return s.done ? SEL_DONE : SEL_SAMPLE;
 }
 
@@ -238,7 +242,7 @@ __device__ __forceinline__ void select_finalize(const float* __restrict__ logits
     SelState s = st[b];
     const int mode = sel_mode(P, step, s);
     if (mode == SEL_PROMPT) {
-        const int next = prompt[b * P.prompt_len + step + 1];
+        const int next = prompt[b * P.pstride + step + 1];
         cur_tok[b] = next < 0 ? s.lang : next;
         return;
     }
@@ -251,7 +255,7 @@ __device__ __forceinline__ void select_finalize(const float* __restrict__ logits
     const float lse_all = r.m_all + __logf(r.s_all);
     if (mode == SEL_SOT) {
         s.nsp = __expf(lg(P.no_speech) - lse_all);
-        int next = prompt[b * P.prompt_len + step + 1];
+        int next = prompt[b * P.pstride + step + 1];
         if (next < 0) {
             next = r.i_text;  // language detection: argmax over language tokens
             // no language won (NaN logits: a NaN never beats the {-inf, INT_MAX} seed of
@@ -297,7 +301,7 @@ __device__ __forceinline__ void select_finalize(const float* __restrict__ logits
         s.penult = s.last;
         s.last = next;
         if (next >= P.tb) s.last_ts = next;
-        if (P.prompt_len + s.n_sampled >= P.max_length) s.done = 1;
+        if (row_plen(P, s) + s.n_sampled >= P.max_length) s.done = 1;
     }
     st[b] = s;
     cur_tok[b] = next;

@@ -1,0 +1,153 @@
+"""Decode sessions (osw_session_*, osw.hip session_step): windows of different clips, seeks,
+prefixes and languages admitted into free decoder slots between chunks of decoder steps,
+each slot's rows on their own step counter.  Every row's arithmetic is the plain decode's
+(rows are independent in every kernel), so each window must decode exactly as it does
+alone through osw_encode_windows + osw_decode_windows: same ids, bit-equal sum_logprob and
+no-speech probability, same language — greedy and beam search."""
+import dataclasses
+
+import pytest
+
+from open_speech_amd import dims as D
+from open_speech_amd import synth, weights
+from open_speech_amd.dims import SpecialTokens
+from open_speech_amd.engine import DecodeConfig, WhisperEngine
+from open_speech_amd.tokenizer import WhisperTokenizer, get_suppressed_tokens
+
+pytestmark = pytest.mark.gpu
+
+
+def _windows(d, n, seed0):
+    st = SpecialTokens.for_vocab(d.n_vocab)
+    out = []
+    for i in range(n):
+        secs = (30.0, 12.5, 47.0)[i % 3]
+        pcm = synth.chirp_clip(seed0 + i, secs)
+        nf = len(pcm) // 160 + 1
+        seek = (0, 700, 1500)[i % 3] if secs > 40 else 0
+        size = min(3000, nf - 1 - seek)
+        prefix = None
+        if i % 4 == 1:
+            prefix = [st.sot_prev] + [100 + (13 * i + 7 * j) % 300 for j in range(3 + i % 5)]
+        lang = None if i % 2 else st.first_lang + (i % 7)
+        out.append(dict(tag=1000 + i, pcm=pcm, seek=seek, segment_size=size, language_token=lang, prefix=prefix,
+                        token_budget=4 + (7 * i) % 19))
+    return out
+
+
+def _alone(eng, w, cfg):
+    eng.log_mel([w["pcm"]])
+    eng.encode([(0, w["seek"], w["segment_size"])])
+    c = dataclasses.replace(cfg, token_budget=(w["token_budget"],))
+    return eng.decode(1, c, prefix=[w["prefix"]] if w["prefix"] else None, languages=[w["language_token"]])[0]
+
+
+def _run_session(eng, cfg, wins, add_in=(1.0,), refill_min=1):
+    """Add the windows in portions (fractions of the list) between steps; collect results."""
+    eng.session_begin(cfg)
+    got = {}
+    try:
+        cut = [0] + [int(round(f * len(wins))) for f in add_in]
+        parts = [wins[a:b] for a, b in zip(cut, cut[1:])]
+        eng.session_add(parts[0])
+        k = 1
+        guard = 0
+        while True:
+            res, active, queued = eng.session_step(max_chunks=2, refill_min=refill_min)
+            for tag, out in res:
+                assert tag not in got
+                got[tag] = out
+            if k < len(parts):
+                eng.session_add(parts[k])
+                k += 1
+                continue
+            if active == 0 and queued == 0:
+                break
+            guard += 1
+            assert guard < 2000
+    finally:
+        eng.session_end()
+    assert sorted(got) == sorted(w["tag"] for w in wins)
+    return got
+
+
+def _compare(eng, cfg, wins, got):
+    for w in wins:
+        r = _alone(eng, w, cfg)
+        g = got[w["tag"]]
+        assert g.tokens == r.tokens, w["tag"]
+        assert g.sum_logprob == r.sum_logprob, w["tag"]
+        assert g.no_speech_prob == r.no_speech_prob, w["tag"]
+        assert g.language == r.language, w["tag"]
+
+
+@pytest.mark.parametrize("beam", [1, 5])
+def test_session_matches_alone_tiny(beam):
+    """17 windows (3 clip lengths, seeks into a 47 s clip, prefixes, detected and fixed
+    languages, budgets 4..22 tokens) through 6 slots, added in three portions while
+    earlier ones decode."""
+    d = D.TINY_TEST
+    eng = WhisperEngine(d, device=0, max_batch=6)
+    try:
+        eng.load_weights(weights.random_weights(d, seed=4321, emb_std=0.5))
+        sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+        cfg = DecodeConfig(suppress_tokens=sup, max_length=64, beam_size=beam)
+        wins = _windows(d, 17, 200)
+        got = _run_session(eng, cfg, wins, add_in=(0.3, 0.6, 1.0))
+        _compare(eng, cfg, wins, got)
+        assert len({len(g.tokens) for g in got.values()}) > 3
+    finally:
+        eng.close()
+
+
+def test_session_no_budget_without_timestamps():
+    """max_length ends the windows; <|notimestamps|> prompts; refill only when 3 slots are free."""
+    d = D.TINY_TEST
+    eng = WhisperEngine(d, device=0, max_batch=4)
+    try:
+        eng.load_weights(weights.random_weights(d, seed=77, emb_std=0.5))
+        sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+        cfg = DecodeConfig(suppress_tokens=sup, max_length=40, without_timestamps=True)
+        wins = _windows(d, 9, 300)
+        for w in wins:
+            w["token_budget"] = 0
+        got = _run_session(eng, cfg, wins, refill_min=3)
+        _compare(eng, cfg, wins, got)
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("beam", [1, 5])
+def test_session_matches_alone_turbo(beam):
+    """large-v3-turbo dims (random weights): 10 windows through 4 slots."""
+    d = D.LARGE_V3_TURBO
+    eng = WhisperEngine(d, device=0, max_batch=4)
+    try:
+        eng.init_random(seed=5)
+        sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+        cfg = DecodeConfig(suppress_tokens=sup, max_length=48, beam_size=beam)
+        wins = _windows(d, 10, 400)
+        got = _run_session(eng, cfg, wins, add_in=(0.5, 1.0))
+        _compare(eng, cfg, wins, got)
+    finally:
+        eng.close()
+
+
+def test_session_rejects_other_calls_and_sampling():
+    d = D.MICRO_TEST
+    eng = WhisperEngine(d, device=0, max_batch=4)
+    try:
+        eng.load_weights(weights.random_weights(d, seed=1, emb_std=0.5))
+        sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+        with pytest.raises(Exception, match="temperature 0"):
+            eng.session_begin(DecodeConfig(suppress_tokens=sup, temperature=0.5, max_length=16))
+        eng.session_begin(DecodeConfig(suppress_tokens=sup, max_length=16))
+        with pytest.raises(Exception, match="session is open"):
+            eng.transcribe_batch([synth.chirp_clip(1, 5.0)], DecodeConfig(suppress_tokens=sup, max_length=16))
+        with pytest.raises(Exception, match="seek out of range"):
+            eng.session_add([dict(tag=1, pcm=synth.chirp_clip(1, 5.0), seek=600, segment_size=10)])
+        eng.session_end()
+        out = eng.transcribe_batch([synth.chirp_clip(1, 5.0)], DecodeConfig(suppress_tokens=sup, max_length=16))
+        assert len(out) == 1
+    finally:
+        eng.close()

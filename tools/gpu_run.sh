@@ -3,6 +3,7 @@
 # usage: tools/gpu_run.sh TAG STEP [STEP ...]    (run through gpurun from the repo root)
 # Every step has its own time limit; the first failing step ends the call.
 #   tests       the whole -m gpu suite                      -> $O/gpu_tests.log
+#   t:FILES     selected gpu test files/ids (commas -> spaces) -> $O/t_N.log
 #   bench       the default bench line                      -> $O/bench.json
 #   prof        one-lane kernel trace of a 3-step bench     -> $O/kernel_summary.txt (+ stats csv)
 #   pmc         FETCH_SIZE / WRITE_SIZE passes (tools/pmc_run.sh) -> $O/pmc/pmc.json
@@ -27,6 +28,10 @@ for s in "$@"; do
     tests)
       timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -rf > $O/gpu_tests.log 2>&1
       rc=$?; tail -5 $O/gpu_tests.log ;;
+    t:*)
+      A=${s#t:}; A=${A//,/ }
+      timeout -k 10 900 python -u -m pytest $A -m gpu -v --timeout 300 --timeout-method thread -rf > $O/t_$i.log 2>&1
+      rc=$?; tail -25 $O/t_$i.log ;;
     bench)
       timeout -k 10 700 python -u bench.py > $O/bench.json 2> $O/bench.err; rc=$?
       [ $rc -eq 0 ] && python3 -c "import json;d=json.load(open('$O/bench.json'));print(d['value'],d['ms_per_step'],d.get('p50_latency_ms_b1'),d.get('beam5',{}).get('value'),d.get('streaming',{}).get('transcriptions_per_s'),d['roofline']['frac'])" ;;

@@ -137,8 +137,14 @@ class HipWhisperBackend:
             # pipelined lanes (runner.py): the lanes of a GPU take turns on the encoder, so
             # one batch encodes while the others decode
             split = os.environ.get("STT_HIP_SPLIT", "1") != "0"
+            # continuous batching (runner._SessionLane): every lane drives a decode session,
+            # windows of any request admitted between chunks of decoder steps
+            continuous = os.environ.get("STT_HIP_CONTINUOUS", "0") != "0"
+            spread = os.environ.get("STT_HIP_SPREAD_MS")
             tok = WhisperTokenizer(src.dims.n_vocab, src.tokenizer_json)
-            runner = BatchRunner(engines, tok, max_wait_ms=wait_ms, gap_ms=gap_ms, split=split)
+            runner = BatchRunner(engines, tok, max_wait_ms=wait_ms, gap_ms=gap_ms, split=split,
+                                 continuous=continuous, refill_min=int(os.environ.get("STT_HIP_REFILL_MIN", "1")),
+                                 spread_ms=float(spread) if spread else None)
             self._models[model_id] = _Model(src, runner, tok, engines)
             now = time.time()
             self._loaded_at[model_id] = now

@@ -35,11 +35,11 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from .segments import ClipResult, TranscribeOptions, transcribe_clips
+from .segments import ClipResult, TranscribeOptions, session_supported, transcribe_clips
 from .tokenizer import WhisperTokenizer, get_suppressed_tokens
 
 
-@dataclass
+@dataclass(eq=False)   # identity: a request holds a numpy clip (deque.remove compares)
 class _Req:
     pcm: np.ndarray
     opts: TranscribeOptions
@@ -187,14 +187,176 @@ class _Worker(threading.Thread):
                     r.fut.set_result(out)
 
 
+class _SessionLane(_Worker):
+    """A lane driving one decode session (osw_session_*, ``continuous`` runners).
+
+    Every request's seek loop advances on its own: its first window is queued into the
+    lane's session when the request is taken, and each finished window is consumed
+    (segments.consume_window) and the clip's next window queued at once, so windows of
+    different requests and different seek positions decode side by side and a finished
+    window's slot is refilled between chunks of 8 decoder steps instead of waiting for
+    the batch's longest window.  A session holds one decode configuration
+    (``TranscribeOptions.key()``): a lane admits only requests of its session's key, and
+    opens a session for another key once its own has drained.  Requests a session cannot
+    hold (segments.session_supported: temperature > 0, max_new_tokens, beam_size > 5)
+    run through the batched seek loop of an idle lane.
+    """
+
+    def _admit(self, key, room: int, idle: bool):
+        """('sess', key, reqs) — requests to add to the session (key: the session's, or a
+        new one when idle); ('batch', reqs); None when the runner closes."""
+        dq, pool = self.dq, self.pool
+        with dq.cv:
+            while True:
+                if dq.closing or not self.alive:
+                    return None
+                if dq.items and room > 0:
+                    if idle:
+                        head = dq.items[0]
+                        if not session_supported(head.opts):
+                            k = head.opts.key()
+                            batch = [r for r in dq.items if r.opts.key() == k][:self.engine.max_batch]
+                            for r in batch:
+                                dq.items.remove(r)
+                            self.inflight = len(batch)
+                            return ("batch", batch)
+                        key = head.opts.key()
+                    else:
+                        now = time.monotonic()
+                        # a request of another key waited max_pace_ms: admit nothing more, so
+                        # this session drains and the lane can switch
+                        if any(r.opts.key() != key and now - r.t_enq > pool.max_pace_ms / 1000.0
+                               for r in dq.items):
+                            return ("sess", key, [])
+                        # spread_ms: an idle sibling takes what waited less than that (a fresh
+                        # session on an idle lane runs beside this one instead of growing it)
+                        idle_sibling = any(w.alive and not w.inflight for w in dq.lanes if w is not self)
+                        if (pool.spread_ms is not None and idle_sibling
+                                and all(now - r.t_enq < pool.spread_ms / 1000.0 for r in dq.items)):
+                            return ("sess", key, [])
+                    take = [r for r in dq.items if r.opts.key() == key][:room]
+                    for r in take:
+                        dq.items.remove(r)
+                    self.inflight += len(take)
+                    if take:
+                        dq.cv.notify_all()
+                    return ("sess", key, take)
+                if not idle:
+                    return ("sess", key, [])
+                dq.cv.wait()
+
+    def run(self) -> None:
+        from .segments import clip_state, consume_window, finish_clip, next_window, session_config
+        pool, eng, tok = self.pool, self.engine, self.pool.tokenizer
+        flights: dict = {}      # tag -> [req, clip state, window]
+        key, is_open, tag = None, False, 0
+
+        def answer(t, exc=None):
+            req, s, _ = flights.pop(t)
+            if not req.fut.done():
+                if exc is None:
+                    req.fut.set_result(finish_clip(s, req.opts, tok))
+                else:
+                    req.fut.set_exception(exc)
+
+        def queue_window(t):
+            req, s, _ = flights[t]
+            if s.done:
+                answer(t)
+                return
+            w = next_window(s, req.opts, tok)
+            w.update(tag=t, pcm=req.pcm)
+            flights[t][2] = w
+            eng.session_add([w])
+
+        while True:
+            idle = not flights
+            if idle and is_open:
+                eng.session_end()
+                is_open = False
+            got = self._admit(key, eng.max_batch - len(flights), idle)
+            if got is None:
+                break
+            try:
+                if got[0] == "batch":
+                    try:
+                        self._run_batch(got[1])
+                    finally:
+                        with self.dq.cv:
+                            self.inflight = 0
+                            self.dq.cv.notify_all()
+                    continue
+                _, k, reqs = got
+                if reqs and not is_open:
+                    eng.session_begin(session_config(reqs[0].opts, pool.suppress_for(reqs[0].opts)))
+                    key, is_open = k, True
+                for r in reqs:
+                    tag += 1
+                    flights[tag] = [r, clip_state(0, r.pcm, r.opts, tok), None]
+                    try:
+                        queue_window(tag)
+                    except Exception as e:  # noqa: BLE001 - this request's window was refused
+                        if pool.is_device_error(e):
+                            raise
+                        answer(tag, e)
+                if not flights:
+                    continue
+                done, _, _ = eng.session_step(max_chunks=1, refill_min=pool.refill_min)
+                for t, out in done:
+                    req, s, w = flights[t]
+                    try:
+                        consume_window(s, w, out, req.opts, tok)
+                        queue_window(t)
+                    except Exception as e:  # noqa: BLE001
+                        if pool.is_device_error(e):
+                            raise
+                        if t in flights:
+                            answer(t, e)
+                with self.dq.cv:
+                    self.inflight = len(flights)
+                    self.dq.cv.notify_all()
+            except Exception as e:  # noqa: BLE001 - forwarded to callers
+                reqs = [f[0] for f in flights.values()] + (list(got[1]) if got[0] == "batch" else [])
+                flights.clear()
+                if is_open:
+                    try:
+                        eng.session_end()
+                    except Exception:  # noqa: BLE001
+                        pass
+                    is_open = False
+                with self.dq.cv:
+                    self.inflight = 0
+                    self.dq.cv.notify_all()
+                if pool.is_device_error(e) and pool.fail_device(self):
+                    for r in reqs:
+                        if not r.fut.done():
+                            pool.submit_req(r)
+                    return
+                for r in reqs:
+                    if not r.fut.done():
+                        r.fut.set_exception(e)
+        if is_open:
+            try:
+                eng.session_end()
+            except Exception:  # noqa: BLE001
+                pass
+        for req, _, _ in flights.values():
+            if not req.fut.done():
+                req.fut.set_exception(RuntimeError("runner closed"))
+
+
 class BatchRunner:
     def __init__(self, engines: list, tokenizer: WhisperTokenizer, max_wait_ms: float = 5.0,
-                 gap_ms: float | None = None, split: bool = True, max_pace_ms: float = 100.0):
+                 gap_ms: float | None = None, split: bool = True, max_pace_ms: float = 100.0,
+                 continuous: bool = False, refill_min: int = 1, spread_ms: float | None = None):
         self.tokenizer = tokenizer
         self.max_wait_ms = max_wait_ms
         self.gap_ms = gap_ms
         self.split = split
         self.max_pace_ms = max_pace_ms
+        self.continuous = continuous
+        self.refill_min = refill_min
+        self.spread_ms = spread_ms
         self._sup_cache: dict = {}
         self._lock = threading.Lock()
         self.queues: list[_DevQueue] = []
@@ -207,7 +369,7 @@ class BatchRunner:
                 by_dev[key] = _DevQueue(dev)
                 self.queues.append(by_dev[key])
             dq = by_dev[key]
-            w = _Worker(self, e, i, dq)
+            w = (_SessionLane if continuous else _Worker)(self, e, i, dq)
             dq.lanes.append(w)
             self.workers.append(w)
         for w in self.workers:

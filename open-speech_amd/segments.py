@@ -25,7 +25,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from .dims import INPUT_STRIDE, N_FRAMES, TIME_PRECISION
+from .dims import HOP_LENGTH, INPUT_STRIDE, N_FRAMES, TIME_PRECISION
 from .engine import DecodeConfig
 from .tokenizer import WhisperTokenizer, compression_ratio
 
@@ -194,6 +194,57 @@ def transcribe_clips(engine, pcm_list: list, opts: TranscribeOptions, tok: Whisp
         code = tok.language_code(s.lang_token) if s.lang_token is not None else (opts.language or "en")
         s.result.language = code
     return [s.result for s in states]
+
+
+# ------------------------------------------------------------ one clip at a time
+# (the runner's decode-session lanes, runner.py: each clip's seek loop advances on its own,
+# its next window queued into the session as soon as the previous one is consumed)
+
+def session_supported(opts: TranscribeOptions) -> bool:
+    """Decode sessions (osw_session_*) hold one decode configuration for every window:
+    temperature 0, beam_size <= 5, and no max_new_tokens (whose max_length depends on
+    each window's prompt length)."""
+    return not (opts.temperature > 0) and opts.max_new_tokens is None and 1 <= int(opts.beam_size) <= 5
+
+
+def session_config(opts: TranscribeOptions, suppress: tuple) -> DecodeConfig:
+    """The session-wide decode configuration (transcribe_clips' per-call one, minus the
+    per-window prefix, language and token budget)."""
+    return DecodeConfig(max_length=448, task=opts.task, language_token=None, suppress_tokens=suppress,
+                        suppress_blank=opts.suppress_blank, without_timestamps=opts.without_timestamps,
+                        max_initial_timestamp_index=int(round(opts.max_initial_timestamp / TIME_PRECISION)),
+                        beam_size=max(1, int(opts.beam_size)), patience=opts.patience,
+                        length_penalty=opts.length_penalty)
+
+
+def clip_state(idx: int, pcm: np.ndarray, opts: TranscribeOptions, tok: WhisperTokenizer) -> _ClipState:
+    """transcribe_clips' per-clip state (log_mel's frame count is len // 160 + 1, the
+    content frames one fewer)."""
+    lang_token = tok.language_token(opts.language) if (opts.language and opts.task == "transcribe") else None
+    init_tokens = tok.encode(" " + opts.initial_prompt.strip()) if opts.initial_prompt else []
+    s = _ClipState(idx=idx, content_frames=len(pcm) // HOP_LENGTH, all_tokens=list(init_tokens),
+                   lang_token=lang_token)
+    s.result.duration = len(pcm) / 16000.0
+    s.done = s.content_frames <= 0
+    return s
+
+
+def next_window(s: _ClipState, opts: TranscribeOptions, tok: WhisperTokenizer) -> dict:
+    """The clip's next window: seek, segment_size, prompt prefix, language, token budget."""
+    prev = s.all_tokens[s.prompt_reset_since:]
+    prefix = ([tok.special.sot_prev] + prev[-(448 // 2 - 1):]) if prev else []
+    size = min(N_FRAMES, s.content_frames - s.seek)
+    budget = int(np.ceil(opts.tokens_per_second * size * FRAME_SEC)) + 2 if opts.tokens_per_second else 0
+    return dict(seek=s.seek, segment_size=size, prefix=prefix, language_token=s.lang_token, token_budget=budget)
+
+
+def consume_window(s: _ClipState, win: dict, out, opts: TranscribeOptions, tok: WhisperTokenizer) -> None:
+    _consume(s, (s.idx, win["seek"], win["segment_size"]), out, opts, tok)
+
+
+def finish_clip(s: _ClipState, opts: TranscribeOptions, tok: WhisperTokenizer) -> ClipResult:
+    s.result.language = tok.language_code(s.lang_token) if s.lang_token is not None else (opts.language or "en")
+    return s.result
 
 
 def _consume(s: _ClipState, win, out, opts: TranscribeOptions, tok: WhisperTokenizer) -> None:

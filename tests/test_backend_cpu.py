@@ -57,6 +57,41 @@ class FakeEngine:
             outs.append(self.script(w, len(self.calls) - 1, prefix[k] if prefix else [], lang))
         return outs
 
+    # decode sessions (runner._SessionLane): a window finishes 1-3 steps after admission
+    def session_begin(self, cfg):
+        assert getattr(self, "_sess", None) is None
+        self._sess = dict(cfg=cfg, q=[], active=[])
+        self.sessions = getattr(self, "sessions", 0) + 1
+
+    def session_add(self, wins):
+        for w in wins:
+            if w["seek"] >= len(w["pcm"]) // 160 + 1:
+                raise ValueError("window seek out of range")
+            self._sess["q"].append(w)
+
+    def session_step(self, max_chunks=1, refill_min=1):
+        time.sleep(getattr(self, "step_sleep", 0.0))
+        s = self._sess
+        while s["q"] and len(s["active"]) < self.max_batch:
+            w = s["q"].pop(0)
+            win = (0, w["seek"], w["segment_size"])
+            prefix = list(w.get("prefix") or [])
+            lang = w.get("language_token")
+            self.calls.append((win, prefix, lang, s["cfg"].task))
+            out = self.script(win, len(self.calls) - 1, prefix, lang)
+            s["active"].append([1 + len(self.calls) % 3, w["tag"], out])
+        self.batches.append(len(s["active"]))
+        done = []
+        for a in s["active"]:
+            a[0] -= 1
+            if a[0] == 0:
+                done.append((a[1], a[2]))
+        s["active"] = [a for a in s["active"] if a[0] > 0]
+        return done, len(s["active"]), len(s["q"])
+
+    def session_end(self):
+        self._sess = None
+
     def close(self):
         self.closed = True
 
@@ -479,5 +514,153 @@ def test_lanes_take_turns_on_the_encoder():
         for r in reqs:
             assert r.fut.result(timeout=30).segments
         assert sorted(n for e in es for n in e.enc_windows) == [1, 4]
+    finally:
+        runner.close()
+
+
+# --------------------------------------------------------------------------- session lanes
+@pytest.fixture
+def continuous(monkeypatch):
+    monkeypatch.setenv("STT_HIP_CONTINUOUS", "1")
+
+
+def test_session_lane_seek_loop(continuous):
+    """The seek loop on a session lane: the second window of the clip starts at the last
+    timestamp with <|startofprev|> + previous tokens and the detected language, as on the
+    batch path (test_seek_loop_conditions_on_previous_text)."""
+    def script(w, i, prefix, lang):
+        clip, seek, size = w
+        if seek == 0:
+            return WindowOutput([TB, 500, 501, TB + 600, TB + 600, 502], -0.5, 0.01, ST.first_lang)
+        return WindowOutput([TB, 600, TB + 30], -0.5, 0.01, ST.first_lang)
+    holder = []
+    b = make_backend(script, holder)
+    r = b.transcribe(wav(30.0), MID, response_format="verbose_json")
+    calls = holder[0].calls
+    assert holder[0].batches and not any(c[0] is None for c in calls)
+    assert calls[0][0] == (0, 0, 3000) and calls[0][1] == []
+    assert calls[1][0] == (0, 1200, 3000 - 1200)
+    assert calls[1][1] == [ST.sot_prev, TB, 500, 501, TB + 600]
+    assert calls[1][2] == ST.first_lang
+    assert [s["seek"] for s in r["segments"]] == [0, 1200]
+    b.unload_model(MID)
+
+
+def test_session_lane_matches_batch_path(monkeypatch):
+    """Many concurrent multi-window requests: the continuous runner's transcripts equal the
+    batch runner's for a script that depends only on the window and its prompt."""
+    def script(w, i, prefix, lang):
+        _, seek, size = w
+        k = (seek // 7 + len(prefix)) % 5
+        toks = [TB, 300 + k, 301 + k, TB + 200 + 50 * k]
+        if k % 2:
+            toks += [TB + 200 + 50 * k, 310 + k]   # unfinished segment: the next window seeks back
+        return WindowOutput(toks, -0.3, 0.01, ST.first_lang + k % 3)
+
+    def run(cont):
+        if cont:
+            monkeypatch.setenv("STT_HIP_CONTINUOUS", "1")
+        else:
+            monkeypatch.delenv("STT_HIP_CONTINUOUS", raising=False)
+        b = make_backend(script)
+        b.load_model(MID)
+        res = [None] * 12
+
+        def call(i):
+            res[i] = b.transcribe(wav(20.0 + 9.0 * i, i), MID, response_format="verbose_json")
+        ts = [threading.Thread(target=call, args=(i,)) for i in range(12)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        b.unload_model(MID)
+        return res
+    a, c = run(False), run(True)
+    assert a == c
+    assert sum(len(r["segments"]) for r in a) > 24
+
+
+def test_session_lane_concurrent_and_fallback(continuous):
+    """Concurrent requests share a lane's session (several windows decode at once);
+    temperature > 0 goes through the batched seek loop of an idle lane."""
+    holder = []
+    b = make_backend(holder=holder)
+    b.load_model(MID)
+    holder[0].step_sleep = 0.01
+    res = [None] * 16
+
+    def call(i):
+        res[i] = b.transcribe(wav(1.0 + 0.1 * i, i), MID, temperature=0.7 if i % 5 == 0 else 0.0)
+    ts = [threading.Thread(target=call, args=(i,)) for i in range(16)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert all(r is not None and "text" in r for r in res)
+    e = holder[0]
+    assert max(e.batches) > 1
+    assert any(c[0] is not None and c[3] == "transcribe" for c in e.calls)
+    b.unload_model(MID)
+
+
+def test_session_lane_bad_window_fails_only_its_request():
+    """A window the session refuses fails its own request; the others complete."""
+    from concurrent.futures import Future
+    from open_speech_amd.runner import BatchRunner, _Req
+    from open_speech_amd.segments import TranscribeOptions
+    from open_speech_amd.tokenizer import WhisperTokenizer
+
+    class Eng(FakeEngine):
+        def session_add(self, wins):
+            if len(wins[0]["pcm"]) == 16000 * 2:
+                raise ValueError("refused")
+            return super().session_add(wins)
+
+    e = Eng(D.MICRO_TEST, 0, 4)
+    runner = BatchRunner([e], WhisperTokenizer(51866), continuous=True)
+    try:
+        opts = TranscribeOptions(beam_size=5, language="en")
+        reqs = [_Req(synth.chirp_clip(i, 2.0 if i == 3 else 3.0), opts, Future()) for i in range(6)]
+        for r in reqs:
+            runner.submit_req(r)
+        for i, r in enumerate(reqs):
+            if i == 3:
+                with pytest.raises(ValueError):
+                    r.fut.result(timeout=30)
+            else:
+                assert r.fut.result(timeout=30).segments
+        assert e.sessions >= 1
+    finally:
+        runner.close()
+
+
+def test_session_lane_device_error_fails_over():
+    """A HIP error in a session step moves the lane's in-flight requests to the other GPU."""
+    from concurrent.futures import Future
+    from open_speech_amd._lib import OswDeviceError
+    from open_speech_amd.runner import BatchRunner, _Req
+    from open_speech_amd.segments import TranscribeOptions
+    from open_speech_amd.tokenizer import WhisperTokenizer
+
+    class Eng(FakeEngine):
+        def __init__(self, device, tag, fail=False):
+            super().__init__(D.MICRO_TEST, device, 8,
+                             lambda w, i, p, l: WindowOutput([TB, 1000 + tag, TB + 50], -1.0, 0.01, ST.first_lang))
+            self.device, self.fail = device, fail
+
+        def session_step(self, max_chunks=1, refill_min=1):
+            if self.fail:
+                raise OswDeviceError("osw_session_step failed (-100): hipErrorLaunchFailure", -100)
+            return super().session_step(max_chunks, refill_min)
+
+    a, b = Eng(0, 1, fail=True), Eng(1, 3)
+    runner = BatchRunner([a, b], WhisperTokenizer(51866), continuous=True)
+    try:
+        reqs = [_Req(synth.chirp_clip(i, 3.0), TranscribeOptions(language="en"), Future()) for i in range(3)]
+        for r in reqs:
+            runner.workers[0].q.put(r)
+        for r in reqs:
+            assert [sg.tokens for sg in r.fut.result(timeout=30).segments] == [[TB, 1003, TB + 50]]
+        assert not runner.workers[0].alive and runner.workers[1].alive
     finally:
         runner.close()

@@ -36,10 +36,13 @@ def _windows(d, n, seed0):
 
 
 def _alone(eng, w, cfg):
+    """The window decoded on its own, twice in one call: a batch-1 greedy decode would pick
+    its tokens in the logits GEMM's epilogue (SelFuse), whose no-speech softmax sums in
+    another order than the select kernel every multi-row decode uses."""
     eng.log_mel([w["pcm"]])
-    eng.encode([(0, w["seek"], w["segment_size"])])
-    c = dataclasses.replace(cfg, token_budget=(w["token_budget"],))
-    return eng.decode(1, c, prefix=[w["prefix"]] if w["prefix"] else None, languages=[w["language_token"]])[0]
+    eng.encode([(0, w["seek"], w["segment_size"])] * 2)
+    c = dataclasses.replace(cfg, token_budget=(w["token_budget"],) * 2)
+    return eng.decode(2, c, prefix=[w["prefix"]] * 2 if w["prefix"] else None, languages=[w["language_token"]] * 2)[0]
 
 
 def _run_session(eng, cfg, wins, add_in=(1.0,), refill_min=1):

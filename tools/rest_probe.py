@@ -3,7 +3,9 @@
 was measured only for streaming): C concurrent callers, each posting R 30 s WAVs (json,
 language None, the backend's default decoding) with exponentially jittered think time
 (mean J ms) between calls.  Prints calls/s and latency percentiles for the gap setting in
-the environment.  usage: rest_probe.py [callers=16] [calls_per_caller=6] [jitter_ms=40]"""
+the environment.  ``mix``: clips of 4-75 s instead (1-3 windows each, windows of different
+lengths and token budgets), the load continuous batching (STT_HIP_CONTINUOUS=1) is for.
+usage: rest_probe.py [callers=16] [calls_per_caller=6] [jitter_ms=40] [mix]"""
 import os
 import sys
 import threading
@@ -26,7 +28,9 @@ MID = "random:large-v3-turbo"
 os.environ.setdefault("STT_HIP_TOKENS_PER_SEC", "4")
 be = HipWhisperBackend()
 be.load_model(MID)
-wavs = [pcm_to_wav(synth.chirp_clip(800 + i, 30.0).tobytes(), 16000) for i in range(8)]
+MIX = len(sys.argv) > 4 and sys.argv[4] == "mix"
+LENS = (4.0, 12.0, 30.0, 45.0, 75.0, 20.0, 8.0, 60.0) if MIX else (30.0,) * 8
+wavs = [pcm_to_wav(synth.chirp_clip(800 + i, s).tobytes(), 16000) for i, s in enumerate(LENS)]
 be.transcribe(audio=wavs[0], model=MID, language=None, response_format="json")  # warm (graphs)
 lat, lock = [], threading.Lock()
 
@@ -49,6 +53,8 @@ for t in ts:
     t.join()
 wall = time.perf_counter() - t0
 gap = os.environ.get("STT_HIP_BATCH_GAP_MS", "1 (default)")
-print(f"gap_ms {gap}: {C} callers x {R} calls, jitter {J:.0f} ms: {len(lat) / wall:.2f} calls/s, "
+mode = "continuous" if os.environ.get("STT_HIP_CONTINUOUS", "0") != "0" else "batch"
+print(f"{mode}{' mix' if MIX else ''} audio {sum(LENS[(i + k) % 8] for i in range(C) for k in range(R)) / wall:.0f} s/s, "
+      f"gap_ms {gap}: {C} callers x {R} calls, jitter {J:.0f} ms: {len(lat) / wall:.2f} calls/s, "
       f"latency p50 {np.median(lat):.0f} ms p95 {np.percentile(lat, 95):.0f} ms", flush=True)
 be.unload_model(MID)

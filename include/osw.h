@@ -223,7 +223,8 @@ int osw_session_add(osw_ctx* ctx, const int16_t* pcm, const int64_t* offsets, in
                     const osw_session_window* windows);
 /* Admit queued windows into free slots (when at least min(refill_min, queued) slots are
  * free, or nothing decodes) and run up to max_chunks chunks of decoder steps, returning
- * after the first chunk in which windows finished.  Their results go to res[0 .. *n_done)
+ * after the first chunk in which windows finished (max_chunks 0: only admit, and wait for
+ * the admitted windows' encoder).  Their results go to res[0 .. *n_done)
  * (res->tokens rows of res->max_tokens), their tags to tags_out; cap >= max_batch.
  * *n_active / *n_queued: windows decoding / waiting after the call. */
 int osw_session_step(osw_ctx* ctx, int32_t max_chunks, int32_t refill_min, osw_window_result* res,

@@ -703,8 +703,14 @@ void encode(osw_ctx* c, const osw_window* wins, int n, const int* slots = nullpt
     struct Restore {
         osw_ctx* c;
         hipStream_t s;
-        ~Restore() { c->stream = s; }
-    } restore{c, dec_stream};
+        bool share;
+        ~Restore() { c->stream = s; c->share_cus = share; }
+    } restore{c, dec_stream, c->share_cus};
+    // the CU reservation for sibling decoders (GemmArgs::share_cus) only for the batched
+    // encoders: the small ones (streaming calls, session admissions) finish sooner on
+    // every CU (OSW_GEMM_GRID=256 in the config-5 simulation: 158.6 -> 164.0 calls/s)
+    static const bool share_small = getenv("OSW_SHARE_SMALL") != nullptr;  // A/B switch
+    if (n < c->baton_min && !share_small) c->share_cus = false;
     if (c->enc_stream) {
         HIPCHK(hipEventRecord(c->enc_in, dec_stream));
         HIPCHK(hipStreamWaitEvent(c->enc_stream, c->enc_in, 0));
@@ -1623,13 +1629,18 @@ int session_step(osw_ctx* c, int max_chunks, int refill_min, osw_window_result* 
     REQUIRE(cap >= S->W, "cap must hold every slot (max_batch)");
     const int beam = S->beam, CH = 8;
     int done = 0;
+    if (max_chunks == 0) {  // admission only: the queued windows' encoder, waited for
+        session_admit(c, refill_min);
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return 0;
+    }
     for (int chunk = 0; chunk < max_chunks && done == 0; ++chunk) {
         session_admit(c, refill_min);
         if (S->active == 0) break;
         int hi = 0;
         for (int i = 0; i < S->W; ++i)
             if (S->slot_tag[i] >= 0) hi = i + 1;
-        hi = std::min(S->W, (hi + 3) / 4 * 4);  // (fewer graph shapes; idle slots' rows are finished)
+        if (hi > 4) hi = std::min(S->W, (hi + 3) / 4 * 4);  // (fewer graph shapes; idle slots' rows are finished)
         const int nb = hi * beam;
         const SelParams& SP = S->SP;
         auto one_step = [&] {
@@ -2032,7 +2043,7 @@ int osw_session_step(osw_ctx* c, int32_t max_chunks, int32_t refill_min, osw_win
         std::lock_guard<std::mutex> lk(c->mu);
         DeviceScope dev_scope_((c->device));
         LaneCall call_(c);
-        *n_done = session_step(c, std::max(1, max_chunks), refill_min, res, tags_out, cap);
+        *n_done = session_step(c, std::max(0, max_chunks), refill_min, res, tags_out, cap);
         *n_active = c->sess->active;
         *n_queued = (int32_t)c->sess->queue.size();
         resolve_events(c);

@@ -211,6 +211,19 @@ class _SessionLane(_Worker):
                 if dq.closing or not self.alive:
                     return None
                 if dq.items and room > 0:
+                    if pool.split and dq.encoding:
+                        # another lane's encoder is running: a busy lane keeps decoding, an
+                        # idle one waits for that encoder (bounded) and then takes everything
+                        # that queued meanwhile — the lanes take turns on the encoder
+                        if not idle:
+                            return ("sess", key, [])
+                        end = time.monotonic() + pool.max_pace_ms / 1000.0
+                        while dq.encoding and not dq.closing and self.alive:
+                            left = end - time.monotonic()
+                            if left <= 0:
+                                break
+                            dq.cv.wait(timeout=left)
+                        continue
                     if idle:
                         head = dq.items[0]
                         if not session_supported(head.opts):
@@ -250,6 +263,7 @@ class _SessionLane(_Worker):
         pool, eng, tok = self.pool, self.engine, self.pool.tokenizer
         flights: dict = {}      # tag -> [req, clip state, window]
         key, is_open, tag = None, False, 0
+        added = False           # windows queued since the last admission
 
         def answer(t, exc=None):
             req, s, _ = flights.pop(t)
@@ -268,6 +282,8 @@ class _SessionLane(_Worker):
             w.update(tag=t, pcm=req.pcm)
             flights[t][2] = w
             eng.session_add([w])
+            nonlocal added
+            added = True
 
         while True:
             idle = not flights
@@ -301,6 +317,18 @@ class _SessionLane(_Worker):
                         answer(tag, e)
                 if not flights:
                     continue
+                if added:
+                    # admission on its own (the encoder, waited for), counted on the GPU's
+                    # queue so that the other lanes take turns with it
+                    added = False
+                    with self.dq.cv:
+                        self.dq.encoding += 1
+                    try:
+                        eng.session_step(max_chunks=0, refill_min=pool.refill_min)
+                    finally:
+                        with self.dq.cv:
+                            self.dq.encoding -= 1
+                            self.dq.cv.notify_all()
                 done, _, _ = eng.session_step(max_chunks=1, refill_min=pool.refill_min)
                 for t, out in done:
                     req, s, w = flights[t]
@@ -318,6 +346,7 @@ class _SessionLane(_Worker):
             except Exception as e:  # noqa: BLE001 - forwarded to callers
                 reqs = [f[0] for f in flights.values()] + (list(got[1]) if got[0] == "batch" else [])
                 flights.clear()
+                added = False
                 if is_open:
                     try:
                         eng.session_end()

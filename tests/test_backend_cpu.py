@@ -80,6 +80,8 @@ class FakeEngine:
             self.calls.append((win, prefix, lang, s["cfg"].task))
             out = self.script(win, len(self.calls) - 1, prefix, lang)
             s["active"].append([1 + len(self.calls) % 3, w["tag"], out])
+        if max_chunks == 0:   # admission only
+            return [], len(s["active"]), len(s["q"])
         self.batches.append(len(s["active"]))
         done = []
         for a in s["active"]:

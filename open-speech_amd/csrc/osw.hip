@@ -1627,7 +1627,12 @@ int session_step(osw_ctx* c, int max_chunks, int refill_min, osw_window_result* 
     REQUIRE(r && r->tokens && r->n_tokens && r->sum_logprob && r->no_speech_prob && r->language && tags,
             "null result argument");
     REQUIRE(cap >= S->W, "cap must hold every slot (max_batch)");
-    const int beam = S->beam, CH = 8;
+    // OSW_SESSION_CHUNK: decoder steps between admission points (default 8, as decode())
+    static const int CH = [] {
+        const char* e = getenv("OSW_SESSION_CHUNK");
+        return e ? std::max(1, std::min(64, atoi(e))) : 8;
+    }();
+    const int beam = S->beam;
     int done = 0;
     if (max_chunks == 0) {  // admission only: the queued windows' encoder, waited for
         session_admit(c, refill_min);
@@ -1659,7 +1664,7 @@ int session_step(osw_ctx* c, int max_chunks, int refill_min, osw_window_result* 
                                               S->o.timestamp_begin, S->o.blank, S->o.first_lang, S->o.n_langs,
                                               S->o.suppress_blank, S->o.without_timestamps,
                                               S->o.max_initial_timestamp_index, beam, SP.num_hyp, SP.max_cand, lp_bits,
-                                              beam, 0, 1, -2};
+                                              beam, 0, 1, -2, CH};
             hipGraphExec_t ge = decode_graph(c, key, one_step, CH);
             trace_graph(c, "launch");
             HIPCHK(hipGraphLaunch(ge, c->stream));

@@ -273,3 +273,122 @@ def test_backend_default_config_matches_oracle_seek_loop(monkeypatch, tmp_path):
         assert got == want
     # the three requests' windows went through more than one lane
     assert sum(1 for e in engines if e._wins) >= 2
+
+
+def test_backend_continuous_matches_oracle_seek_loop(monkeypatch, tmp_path):
+    """Continuous batching as deployed (STT_HIP_CONTINUOUS=1, runner._SessionLane): the
+    backend's defaults otherwise (beam 5, 3 lanes, max batch 16), four concurrent requests
+    (75, 61, 47 and 12 s WAVs) arriving while earlier ones decode, so windows of different
+    requests and seek positions share a lane's decode session and join it between chunks
+    of steps.  Every window a session admitted is recorded (prompt, result); its encoder
+    output is recomputed on a separate context (a window's encoder output does not depend
+    on its batch: test_tile_sizes_bit_identical) and each request's windows are replayed
+    through the oracle's seek loop with the oracle's beam search (width 5): every prompt
+    and every window's ids must equal the oracle's, each response's segments the
+    oracle's."""
+    import hashlib
+
+    import tokfix
+    from oracle import decode as odec
+    from oracle import seek as oseek
+    from oracle.model import WhisperOracle
+    from open_speech_amd import dims as D
+    from open_speech_amd import model_store
+    from open_speech_amd.engine import WhisperEngine
+    from open_speech_amd.tokenizer import WhisperTokenizer, get_suppressed_tokens
+
+    for k in ("STT_HIP_BEAM_SIZE", "STT_HIP_LANES", "STT_HIP_MAX_BATCH", "STT_HIP_BATCH_GAP_MS",
+              "STT_HIP_BATCH_WAIT_MS", "STT_HIP_TOKENS_PER_SEC", "STT_HIP_SPREAD_MS", "STT_HIP_REFILL_MIN"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("STT_HIP_GPUS", "0")
+    monkeypatch.setenv("STT_HIP_CONTINUOUS", "1")
+
+    added, done, shared = {}, {}, []
+    lock = threading.Lock()
+
+    class Recorder:
+        def __init__(self, eng):
+            self.eng = eng
+            self.tags = {}
+
+        def __getattr__(self, k):
+            return getattr(self.eng, k)
+
+        def sibling(self, max_batch=None):
+            return Recorder(self.eng.sibling(max_batch))
+
+        def session_begin(self, cfg):
+            assert cfg.beam_size == 5, "the backend's default decoding is beam search width 5"
+            return self.eng.session_begin(cfg)
+
+        def session_add(self, wins):
+            with lock:
+                for w in wins:
+                    h = hashlib.sha1(np.asarray(w["pcm"], np.int16).tobytes()).hexdigest()
+                    self.tags[w["tag"]] = (h, w["seek"], w["segment_size"])
+                    added[(h, w["seek"], w["segment_size"])] = list(w["prefix"] or [])
+            return self.eng.session_add(wins)
+
+        def session_step(self, max_chunks=1, refill_min=1):
+            res, active, queued = self.eng.session_step(max_chunks, refill_min)
+            with lock:
+                shared.append(active + len(res))
+                for tag, out in res:
+                    done[self.tags[tag]] = out
+            return res, active, queued
+
+    def factory(dims, gpu, max_batch):
+        return Recorder(WhisperEngine(dims, device=gpu, max_batch=max_batch))
+
+    mid = tokfix.make_hf_model_dir(str(tmp_path / "micro_hf"), D.MICRO_TEST)
+    b = HipWhisperBackend(engine_factory=factory)
+    b.load_model(mid)
+    clips = [synth.chirp_clip(61 + i, s) for i, s in enumerate((75.0, 61.0, 47.0, 12.0))]
+    res = [None] * len(clips)
+    try:
+        def go(i):
+            res[i] = b.transcribe(synth.to_wav_bytes(clips[i]), mid, response_format="verbose_json")
+        ts = [threading.Thread(target=go, args=(i,)) for i in range(len(clips))]
+        for t in ts:
+            t.start()
+            time.sleep(0.02)
+        for t in ts:
+            t.join(timeout=600)
+    finally:
+        b.unload_model(mid)
+    assert all(r is not None for r in res)
+    assert max(shared) >= 2, "windows of different requests decoded in one session"
+    src = model_store.resolve(mid)
+    d, w = src.dims, model_store.load_weights(src)
+    tok = WhisperTokenizer(d.n_vocab, src.tokenizer_json)
+    st = tok.special
+    sup = get_suppressed_tokens(tok, [-1])
+    orc = WhisperOracle(d, w, fp16=True)
+    eng = WhisperEngine(d, device=0, max_batch=1)
+    try:
+        eng.load_weights(w)
+        for pcm, r in zip(clips, res):
+            h = hashlib.sha1(pcm.tobytes()).hexdigest()
+            eng.log_mel([pcm])
+            lang = {}
+
+            def decode_window(seek, size, prompt_toks):
+                key = (h, seek, size)
+                assert key in done, f"{len(pcm)} samples, window {seek}: not decoded by a session"
+                eng.encode([(0, seek, size)])
+                enc = eng.encoder_output(0)
+                o = odec.beam_from_encoder(orc, orc.cross_kv(enc), st, language=lang.get("tok"),
+                                           prev_tokens=prompt_toks[1:], opts=odec.DecodeOptions(suppress_tokens=sup),
+                                           beam=odec.BeamOptions(beam_size=5))
+                lang.setdefault("tok", o.language)
+                go_ = done[key]
+                assert added[key] == prompt_toks, f"{len(pcm)} samples, window {seek}: prompt differs"
+                assert go_.tokens == o.tokens, f"{len(pcm)} samples, window {seek}: ids differ from the oracle's"
+                return go_.tokens, go_.sum_logprob, go_.no_speech_prob
+
+            wins = oseek.seek_loop(decode_window, (len(pcm) + 160) // 160, st, tok.decode)
+            want = [(round(a, 6), round(e, 6), t) for x in wins for a, e, t in x.segments]
+            got = [(round(s["start"], 6), round(s["end"], 6), s["tokens"]) for s in r["segments"]]
+            assert got == want
+    finally:
+        eng.close()

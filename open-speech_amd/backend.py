@@ -138,8 +138,11 @@ class HipWhisperBackend:
             # one batch encodes while the others decode
             split = os.environ.get("STT_HIP_SPLIT", "1") != "0"
             # continuous batching (runner._SessionLane): every lane drives a decode session,
-            # windows of any request admitted between chunks of decoder steps
-            continuous = os.environ.get("STT_HIP_CONTINUOUS", "0") != "0"
+            # windows of any request admitted between chunks of decoder steps.  Mixed-length
+            # REST load (tools/rest_probe.py mix, 16 callers): 52.8 -> 67.3 calls/s, p50
+            # 236 -> 148 ms; config 5 within noise of batch-at-a-time (165.7 / 169.0 calls/s,
+            # gpurun_out/r05_s3, r05_s4).  STT_HIP_CONTINUOUS=0: batch at a time.
+            continuous = os.environ.get("STT_HIP_CONTINUOUS", "1") != "0"
             spread = os.environ.get("STT_HIP_SPREAD_MS")
             tok = WhisperTokenizer(src.dims.n_vocab, src.tokenizer_json)
             runner = BatchRunner(engines, tok, max_wait_ms=wait_ms, gap_ms=gap_ms, split=split,

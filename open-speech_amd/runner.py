@@ -21,6 +21,13 @@ of 4 — encode 4, decode 4, nothing overlapping — into staggered batches that
 on the encoder while the other batches decode.  With a deep queue (REST load) the
 batches are ``max_batch`` anyway.
 
+Continuous batching (``continuous``, the backend's default): every lane drives a decode
+session instead (``_SessionLane``, osw_session_*): a request's windows are queued into
+the session one at a time as its seek loop advances, free decoder slots are refilled
+between chunks of 8 decoder steps, so a request arriving mid-batch starts within a chunk
+and a batch costs what its windows' own lengths cost.  Lanes take turns on the encoder
+the same way (a session's admission is an encoder call counted on the GPU's queue).
+
 A lane whose GPU fails marks every lane of that GPU dead, moves the GPU's queued
 requests to the other GPUs and re-queues there the requests of its batch that are
 still unanswered.

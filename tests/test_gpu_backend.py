@@ -110,6 +110,7 @@ def test_backend_verbose_json_matches_oracle_seek_loop(monkeypatch, tmp_path, va
     else:
         mid, prompt = tokfix.make_hf_model_dir(str(tmp_path / "micro_hf"), D.MICRO_TEST), "  Budget review, part two. "
     monkeypatch.setenv("STT_HIP_BEAM_SIZE", "1")
+    monkeypatch.setenv("STT_HIP_CONTINUOUS", "0")  # batch at a time: the recorder sees encode/decode
     monkeypatch.setenv("STT_HIP_MAX_BATCH", "2")
     monkeypatch.setenv("STT_HIP_GPUS", "0")
     monkeypatch.setenv("STT_HIP_LANES", "1")  # one lane: every window goes through the recorder
@@ -167,7 +168,7 @@ def test_backend_verbose_json_matches_oracle_seek_loop(monkeypatch, tmp_path, va
 
 
 def test_backend_default_config_matches_oracle_seek_loop(monkeypatch, tmp_path):
-    """The backend as deployed: its defaults (STT_HIP_BEAM_SIZE 5 = the reference's
+    """The batch-at-a-time backend (STT_HIP_CONTINUOUS=0), its defaults otherwise (STT_HIP_BEAM_SIZE 5 = the reference's
     beam_size, src/backends/faster_whisper.py:237; 3 lanes per GPU; max batch 16; the
     batcher's 1 ms gap), three concurrent requests (75, 61 and 47 s WAVs) so the batcher
     spreads windows over the lanes and batches windows of different clips.  Every lane is
@@ -191,6 +192,7 @@ def test_backend_default_config_matches_oracle_seek_loop(monkeypatch, tmp_path):
               "STT_HIP_BATCH_WAIT_MS", "STT_HIP_TOKENS_PER_SEC"):
         monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("STT_HIP_GPUS", "0")
+    monkeypatch.setenv("STT_HIP_CONTINUOUS", "0")  # batch at a time (the continuous form: below)
 
     calls = []              # (clip hash, seek, size, prompt, output, encoder output) over every lane
     lock = threading.Lock()
@@ -276,8 +278,8 @@ def test_backend_default_config_matches_oracle_seek_loop(monkeypatch, tmp_path):
 
 
 def test_backend_continuous_matches_oracle_seek_loop(monkeypatch, tmp_path):
-    """Continuous batching as deployed (STT_HIP_CONTINUOUS=1, runner._SessionLane): the
-    backend's defaults otherwise (beam 5, 3 lanes, max batch 16), four concurrent requests
+    """Continuous batching as deployed (the default, STT_HIP_CONTINUOUS=1, runner._SessionLane):
+    the backend's defaults (beam 5, 3 lanes, max batch 16), four concurrent requests
     (75, 61, 47 and 12 s WAVs) arriving while earlier ones decode, so windows of different
     requests and seek positions share a lane's decode session and join it between chunks
     of steps.  Every window a session admitted is recorded (prompt, result); its encoder

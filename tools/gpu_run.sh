@@ -13,6 +13,7 @@
 #   repro       tools/graph_prof_repro (mode 2) under a rocprofv3 kernel trace -> $O/repro.log
 #   bench:ARGS  bench.py with extra args (commas -> spaces) -> $O/bench_N.json
 #   py:SCRIPT,ARGS  python3 SCRIPT ARGS                     -> $O/py_N.txt
+#   rprof:SCRIPT,ARGS  the same under a rocprofv3 kernel trace -> $O/rprof_N.txt, rprof_N.summary.txt
 #   env:A=1,B=2 / unenv:A,B   set / clear environment variables for the following steps
 # stream and streamprof write $O/stream[_prof]_N.json when run more than once (N = step index)
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -65,6 +66,12 @@ for s in "$@"; do
       A=${s#bench:}; A=${A//,/ }
       timeout -k 10 600 python -u bench.py $A > $O/bench_$i.json 2> $O/bench_$i.err; rc=$?
       head -c 600 $O/bench_$i.json; echo ;;
+    rprof:*)
+      A=${s#rprof:}; A=${A//,/ }
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rprof_$i -o run -- python3 -u $A > $O/rprof_$i.txt 2>&1; rc=$?
+      tail -8 $O/rprof_$i.txt
+      [ $rc -eq 0 ] && python3 tools/kstats.py $O/rprof_$i/run_kernel_stats.csv 25 > $O/rprof_$i.summary.txt
+      rm -f $O/rprof_$i/run_kernel_trace.csv ;;
     py:*)
       A=${s#py:}; A=${A//,/ }
       timeout -k 10 600 python3 -u $A > $O/py_$i.txt 2>&1; rc=$?

@@ -5,14 +5,12 @@
 // construction; tests/test_gpu_parity.py::test_batch_equals_single).
 //
 // Per row r:  x' = x + bias + Σ_k part[k][r]   (or the embedding tok_emb[tok] + pos_emb[pos])
-//             y  = (x' - mean) * rstd * g + b   (eps 1e-5, fp32)
-// The statistics are computed in 64-column blocks and combined (ln_block / ln_combine
-// below), so a kernel that holds only some 64-column blocks of a row (the last arriver of a
-// decoder projection, gemm.hip) produces the same statistics as one that holds the row.
+//             y  = (x' - mean) * rstd * g + b   (two-pass variance, eps 1e-5, fp32)
 // 256 threads; thread t owns columns 4t..4t+3 (one 16-B piece) and 1024 + t (D <= 1280).
 // Every slab piece of a row is loaded before any is added (8 slabs per batch, clamped
 // addresses, the surplus added as exact zeros), so a row costs one memory round trip
-// per 8 slabs; the sums run in slab order.
+// per 8 slabs; the sums run in slab order, the thread's 5 columns in order, then
+// wave_sum, then the 4 wave partials in order.
 #pragma once
 #include "common.h"
 #include "decode.h"
@@ -38,43 +36,8 @@ struct ResLnArgs {
     int pos_row;        // 1: row r's position is pos[r] (row refill), 0: every row's is pos[0]
 };
 
-// LayerNorm statistics in 64-column blocks (the pairwise combination of Chan, Golub and
-// LeVeque): block b of a row, one column per lane of a wave,
-//   m_b = wave_sum(x) / 64,  q_b = wave_sum((x - m_b)^2)
-// and the row from its D/64 blocks in order,
-//   mean = (Σ_b m_b) / nb,  M2 = Σ_b q_b + 64 Σ_b (m_b - mean)^2,  rstd = rsqrt(M2 / D + eps).
-// As accurate as the two-pass variance; every kernel that normalises a decoder row calls
-// these two functions, so the statistics are bit-identical whichever kernel made them.
-__device__ __forceinline__ float2 ln_block(float x) {
-#pragma clang fp contract(off)
-    const float m = wave_sum(x) * (1.f / 64.f);
-    const float d = x - m;
-    return make_float2(m, wave_sum(d * d));
-}
-// st: the row's nb block statistics in order; returns (mean, rstd)
-template <class Load>
-__device__ __forceinline__ float2 ln_combine(Load st, int nb) {
-#pragma clang fp contract(off)
-    float s = 0.f;
-    for (int b = 0; b < nb; ++b) s += st(b).x;
-    const float mean = s / (float)nb;
-    float q = 0.f, e = 0.f;
-    for (int b = 0; b < nb; ++b) {
-        const float2 v = st(b);
-        q += v.y;
-        const float dm = v.x - mean;
-        e = fmaf(dm, dm, e);
-    }
-    const float var = (q + 64.f * e) / (float)(64 * nb);
-    return make_float2(mean, rsqrtf(var + 1e-5f));
-}
-__device__ __forceinline__ float ln_apply(float x, float2 mr, float g, float b) {
-#pragma clang fp contract(off)
-    return fmaf((x - mr.x) * mr.y, g, b);
-}
-
 // rows r0 .. r0+nr-1 (nr <= NR); emit(r, c, y) receives every LayerNorm output;
-// write_x: this workgroup stores x'.  red: LDS scratch of resln_scratch(NR, D) floats.  KB: slab
+// write_x: this workgroup stores x'.  red: LDS scratch of 2 * NR * 4 floats.  KB: slab
 // loads per batch (the sums do not depend on it: the padding adds exact zeros).
 template <int NR, int KB, class Emit>
 __device__ __forceinline__ void resln_rows(const ResLnArgs& A, int r0, int nr, bool write_x, float* red, Emit emit) {
@@ -139,38 +102,50 @@ __device__ __forceinline__ void resln_rows(const ResLnArgs& A, int r0, int nr, b
         }
         if (h1) v[r][4] = a1;
     }
-    // the row image in LDS, then one 64-column block per wave at a time (ln_block), the
-    // block statistics in LDS, the row's (mean, rstd) from them in order (ln_combine)
-    float* img = red;                       // [NR][D]
-    float2* bst = (float2*)(red + NR * D);  // [NR][D / 64]
-    const int nb = D / 64;
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
-        if (r >= nr) break;
-        if (h4) *(f32x4*)(img + r * D + c4) = f32x4{v[r][0], v[r][1], v[r][2], v[r][3]};
-        if (h1) img[r * D + c1] = v[r][4];
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) s += v[r][i];
+        s = wave_sum(s);
+        if (l == 0) red[r * 4 + w] = s;
     }
     __syncthreads();
-    for (int j = w; j < nr * nb; j += 4) {
-        const float2 st = ln_block(img[(j / nb) * D + (j % nb) * 64 + l]);
-        if (l == 0) bst[j] = st;
+    float mean[NR], rstd[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        mean[r] = (((red[r * 4 + 0] + red[r * 4 + 1]) + red[r * 4 + 2]) + red[r * 4 + 3]) / D;
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+            if (i < 4 ? h4 : h1) {
+                const float d = v[r][i] - mean[r];
+                q = fmaf(d, d, q);
+            }
+        q = wave_sum(q);
+        if (l == 0) red[(NR + r) * 4 + w] = q;
     }
     __syncthreads();
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const float q = (((red[(NR + r) * 4 + 0] + red[(NR + r) * 4 + 1]) + red[(NR + r) * 4 + 2]) +
+                         red[(NR + r) * 4 + 3]);
+        rstd[r] = rsqrtf(q / D + 1e-5f);
+    }
     const f32x4 g4 = *(const f32x4*)(A.g + c4), b4 = *(const f32x4*)(A.b + c4);
     const float g1 = A.g[c1], b1 = A.b[c1];
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
         if (r >= nr) break;
-        const float2 mr = ln_combine([&](int b) { return bst[r * nb + b]; }, nb);
         if (h4)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) emit(r, c4 + i, ln_apply(v[r][i], mr, g4[i], b4[i]));
-        if (h1) emit(r, c1, ln_apply(v[r][4], mr, g1, b1));
+            for (int i = 0; i < 4; ++i) emit(r, c4 + i, fmaf((v[r][i] - mean[r]) * rstd[r], g4[i], b4[i]));
+        if (h1) emit(r, c1, fmaf((v[r][4] - mean[r]) * rstd[r], g1, b1));
     }
 }
 
 // LDS scratch (floats) resln_rows needs for NR rows of D columns
-constexpr int resln_scratch(int NR, int D) { return NR * D + NR * (D / 64) * 2; }
+constexpr int resln_scratch(int NR, int D) { return (void)D, 2 * NR * 4; }
 
 // Operand prologue of the small-batch decoder GEMM (gemm.hip): the workgroup builds its
 // activation rows itself instead of loading them, so the kernel that produced them

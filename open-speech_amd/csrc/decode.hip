@@ -816,11 +816,10 @@ static_assert(BEAM_SLICES * 256 * TOPK_VPT >= SEL_SPLIT * 4096, "osw.hip admits 
 template <bool FAST>
 __device__ __forceinline__ void beam_slice_body(const float* __restrict__ logits, const SelParams& P, int step,
                                                 const unsigned* __restrict__ supmask, const SelState& s,
-                                                SelPart* __restrict__ parts, BeamCand* __restrict__ cand, int b,
-                                                int sl) {
+                                                SelPart* __restrict__ parts, BeamCand* __restrict__ cand) {
     __shared__ ArgMax red[2][4];
     __shared__ SelPart wp[4];
-    const int tid = threadIdx.x;
+    const int b = blockIdx.x, sl = blockIdx.y, tid = threadIdx.x;
     const int K2 = 2 * P.beam;
     BeamCand* outA = cand + ((int64_t)b * BEAM_SLICES + sl) * 2 * MAXK2;
     BeamCand* outB = outA + MAXK2;
@@ -995,10 +994,7 @@ __device__ __forceinline__ void beam_slice_body(const float* __restrict__ logits
 // MODE 0: greedy rows, 1: sampling rows (temperature > 0), 2: beam rows.  Each launch
 // compiles only its own path: the greedy kernel carries neither the Gumbel keys nor the
 // beam candidate lists (47 VGPRs, so it fits beside another lane's encoder workgroup).
-// SPW: slices per workgroup (grid (rows, SEL_SPLIT / SPW)): a workgroup walks SPW
-// consecutive slices with the same per-slice code, so the records (and every result) do
-// not depend on SPW; many beam rows launch fewer, longer workgroups.
-template <int MODE, int SPW = 1>
+template <int MODE>
 // waves_per_eu(6): <= 80 VGPRs (the beam form needs 81 unbounded), so it fits beside an encoder GEMM workgroup
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void select_kernel(const float* __restrict__ logits, SelParams P,
                                                      int* __restrict__ pos_ptr, const unsigned* __restrict__ supmask,
@@ -1007,30 +1003,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void s
                                                      int* __restrict__ tokens, int max_tokens,
                                                      int* __restrict__ arrive, int* __restrict__ ticket, int bump,
                                                      BeamCand* __restrict__ cand) {
-    const int b = blockIdx.x;
-    const int step = pos_ptr[P.pos_row ? b : 0];
+    const int step = pos_ptr[P.pos_row ? blockIdx.x : 0];
     if ((MODE == 2 || MODE == 3) && P.beam > 1) {
-        const SelState s = st[b];
+        const SelState s = st[blockIdx.x];
         if (sel_mode(P, step, s) == SEL_SAMPLE) {  // the same for every slice of the row
             // beam rows' sampling steps: statistics + candidates in one pass; nothing to
             // finalise here (beam_update picks), so no ticket
-            if (step == row_plen(P, s) - 1 && b % P.beam != 0) return;  // only the prompt hypothesis expands
-            for (int j = 0; j < SPW; ++j) {
-                if (j) __syncthreads();  // the previous slice's LDS records are read
-                beam_slice_body<MODE == 2>(logits, P, step, supmask, s, parts, cand, b, blockIdx.y * SPW + j);
-            }
+            if (step == row_plen(P, s) - 1 && blockIdx.x % P.beam != 0) return;  // only the prompt hypothesis expands
+            beam_slice_body<MODE == 2>(logits, P, step, supmask, s, parts, cand);
             return;
         }
     }
-    for (int j = 0; j < SPW; ++j) {
-        if (j) __syncthreads();
-        select_partial_body<MODE == 1>(logits, P, step, supmask, st, parts, b, blockIdx.y * SPW + j);
-    }
+    select_partial_body<MODE == 1>(logits, P, step, supmask, st, parts);
     __shared__ int last;
     __shared__ SelPart rp[SEL_SPLIT];
+    const int b = blockIdx.x;
     if (threadIdx.x == 0) {
         __builtin_amdgcn_s_waitcnt(0);  // this slice's part stores are complete at device scope
-        last = __hip_atomic_fetch_add(ticket + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.y - 1;
+        last = __hip_atomic_fetch_add(ticket + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == SEL_SPLIT - 1;
         if (last) __hip_atomic_store(ticket + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
     }
     __syncthreads();
@@ -1437,29 +1427,10 @@ void launch_select(const float* logits, int rows, int* pos, const SelParams& P, 
     if (P.beam > 1 && pops_only)
         select_kernel<3><<<grid, 256, 0, s>>>(logits, P, pos, supmask, prompt, (SelPart*)sel_parts, st, cur_tok, tokens,
                                                max_tokens, arrive, arrive + 1, bump ? 1 : 0, (BeamCand*)cand);
-    else if (P.beam > 1) {
-        // OSW_SEL_SPW: slices per workgroup for >= OSW_SEL_SPW_ROWS beam rows (same records)
-        static const int spw = [] {
-            const char* e = std::getenv("OSW_SEL_SPW");
-            const int v = e ? atoi(e) : 1;
-            return v == 2 || v == 4 || v == 8 || v == 16 ? v : 1;
-        }();
-        static const int spw_rows = [] {
-            const char* e = std::getenv("OSW_SEL_SPW_ROWS");
-            return e ? atoi(e) : 64;
-        }();
-        const int w = rows >= spw_rows ? spw : 1;
-        const dim3 g2(rows, SEL_SPLIT / w);
-        auto go = [&](auto k) {
-            k<<<g2, 256, 0, s>>>(logits, P, pos, supmask, prompt, (SelPart*)sel_parts, st, cur_tok, tokens, max_tokens,
-                                 arrive, arrive + 1, bump ? 1 : 0, (BeamCand*)cand);
-        };
-        if (w == 2) go(select_kernel<2, 2>);
-        else if (w == 4) go(select_kernel<2, 4>);
-        else if (w == 8) go(select_kernel<2, 8>);
-        else if (w == 16) go(select_kernel<2, 16>);
-        else go(select_kernel<2, 1>);
-    } else if (P.inv_temp > 0.f)
+    else if (P.beam > 1)
+        select_kernel<2><<<grid, 256, 0, s>>>(logits, P, pos, supmask, prompt, (SelPart*)sel_parts, st, cur_tok, tokens,
+                                               max_tokens, arrive, arrive + 1, bump ? 1 : 0, (BeamCand*)cand);
+    else if (P.inv_temp > 0.f)
         select_kernel<1><<<grid, 256, 0, s>>>(logits, P, pos, supmask, prompt, (SelPart*)sel_parts, st, cur_tok, tokens,
                                                max_tokens, arrive, arrive + 1, bump ? 1 : 0, (BeamCand*)cand);
     else

@@ -123,13 +123,12 @@ __device__ __forceinline__ SelPart load_part(const SelPart* src) {
     return r;
 }
 
-// 256 threads: vocabulary slice sl of row b
+// grid (B, SEL_SPLIT), 256 threads: one vocabulary slice of one row
 template <bool SAMPLE>
 __device__ __forceinline__ void select_partial_body(const float* __restrict__ logits, const SelParams& P, int step,
                                                     const unsigned* __restrict__ supmask,
-                                                    const SelState* __restrict__ st, SelPart* __restrict__ parts,
-                                                    int b, int sl) {
-    const int tid = threadIdx.x;
+                                                    const SelState* __restrict__ st, SelPart* __restrict__ parts) {
+    const int b = blockIdx.x, sl = blockIdx.y, tid = threadIdx.x;
     const SelState s = st[b];
     const int mode = sel_mode(P, step, s);
     if (mode == SEL_PROMPT || mode == SEL_DONE) return;

@@ -3,6 +3,7 @@
 # usage: tools/gpu_run.sh TAG STEP [STEP ...]    (run through gpurun from the repo root)
 # Every step has its own time limit; the first failing step ends the call.
 #   tests       the whole -m gpu suite                      -> $O/gpu_tests.log
+#   smoke       __graft_entry__.smoke()                     -> $O/smoke.log
 #   t:FILES     selected gpu test files/ids (commas -> spaces) -> $O/t_N.log
 #   bench       the default bench line                      -> $O/bench.json
 #   prof        one-lane kernel trace of a 3-step bench     -> $O/kernel_summary.txt (+ stats csv)
@@ -29,6 +30,9 @@ for s in "$@"; do
     tests)
       timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -rf > $O/gpu_tests.log 2>&1
       rc=$?; tail -5 $O/gpu_tests.log ;;
+    smoke)
+      timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
+      rc=$?; tail -3 $O/smoke.log ;;
     t:*)
       A=${s#t:}; A=${A//,/ }
       timeout -k 10 900 python -u -m pytest $A -m gpu -v --timeout 300 --timeout-method thread -rf > $O/t_$i.log 2>&1

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-step kernel breakdown of the batch-1 greedy decode from a rocprofv3 kernel trace of
-`bench.py --lanes 1 --steps 1 --latency-repeats N` (tools/run/r04_aj.sh): kernels grouped by
+`bench.py --lanes 1 --steps 1 --latency-repeats N` (tools/gpu_run.sh b1): kernels grouped by
 (name, grid), keeping the groups whose launch count is a multiple of the batch-1 step count
 (the 64-window step's launches have other grids), with the mean duration and the launches
 per step.  usage: b1_breakdown.py run_kernel_trace.csv[.gz] steps"""

@@ -58,7 +58,7 @@ class FakeEngine:
         return outs
 
     # decode sessions (runner._SessionLane): a window finishes 1-3 steps after admission
-    def session_begin(self, cfg):
+    def session_begin(self, cfg, async_admit=False):
         assert getattr(self, "_sess", None) is None
         self._sess = dict(cfg=cfg, q=[], active=[])
         self.sessions = getattr(self, "sessions", 0) + 1

@@ -35,7 +35,7 @@ for s in "$@"; do
       rc=$?; tail -3 $O/smoke.log ;;
     t:*)
       A=${s#t:}; A=${A//,/ }
-      timeout -k 10 900 python -u -m pytest $A -m gpu -v --timeout 300 --timeout-method thread -rf > $O/t_$i.log 2>&1
+      timeout -k 10 900 python -u -m pytest $A -m gpu -v --timeout ${T_TIMEOUT:-300} --timeout-method thread -rf --durations=5 > $O/t_$i.log 2>&1
       rc=$?; tail -25 $O/t_$i.log ;;
     bench)
       timeout -k 10 700 python -u bench.py > $O/bench.json 2> $O/bench.err; rc=$?

@@ -365,7 +365,11 @@ class _SessionLane(_Worker):
                     self.inflight = len(flights)
                     self.dq.cv.notify_all()
             except Exception as e:  # noqa: BLE001 - forwarded to callers
-                reqs = [f[0] for f in flights.values()] + (list(got[1]) if got[0] == "batch" else [])
+                # the requests in flight and the ones taken this round (not all in flights yet)
+                reqs = [f[0] for f in flights.values()]
+                for r in (got[1] if got[0] == "batch" else got[2]):
+                    if not any(r is q for q in reqs):
+                        reqs.append(r)
                 flights.clear()
                 added = False
                 if is_open:

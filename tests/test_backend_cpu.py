@@ -666,3 +666,27 @@ def test_session_lane_device_error_fails_over():
         assert not runner.workers[0].alive and runner.workers[1].alive
     finally:
         runner.close()
+
+
+def test_session_lane_error_before_flight_fails_taken_requests():
+    """An error while opening the session (before the taken requests are in flight) fails
+    those requests instead of dropping them (a request is never left unanswered)."""
+    from concurrent.futures import Future
+    from open_speech_amd.runner import BatchRunner, _Req
+    from open_speech_amd.segments import TranscribeOptions
+    from open_speech_amd.tokenizer import WhisperTokenizer
+
+    class Eng(FakeEngine):
+        def session_begin(self, cfg, async_admit=False):
+            raise ValueError("cannot open")
+
+    runner = BatchRunner([Eng(D.MICRO_TEST, 0, 4)], WhisperTokenizer(51866), continuous=True)
+    try:
+        reqs = [_Req(synth.chirp_clip(i, 3.0), TranscribeOptions(language="en"), Future()) for i in range(3)]
+        for r in reqs:
+            runner.submit_req(r)
+        for r in reqs:
+            with pytest.raises(ValueError, match="cannot open"):
+                r.fut.result(timeout=10)
+    finally:
+        runner.close()

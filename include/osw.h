@@ -217,11 +217,7 @@ typedef struct osw_session_window {
     int32_t n_prefix;         /* previous-text prompt tokens before <|startoftranscript|> */
     const int32_t* prefix;    /* <|startofprev|> and the previous tokens, or NULL */
 } osw_session_window;
-/* flags: OSW_SESSION_ASYNC_ADMIT -- a queued window's encoder runs on a side stream while
- * the session keeps decoding; the window joins at the first chunk boundary after it finished
- * (the decoder never waits for an encoder unless nothing else decodes). */
-#define OSW_SESSION_ASYNC_ADMIT 1
-int osw_session_begin(osw_ctx* ctx, const osw_decode_opts* opts, int32_t flags);
+int osw_session_begin(osw_ctx* ctx, const osw_decode_opts* opts);
 /* Queue n windows; window i reads clip pcm[offsets[i], offsets[i+1]) (host int16, copied). */
 int osw_session_add(osw_ctx* ctx, const int16_t* pcm, const int64_t* offsets, int32_t n,
                     const osw_session_window* windows);

@@ -13,7 +13,6 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("OSW_LIB", os.path.join(_HERE, "lib", "libosw_hip.so"))
 
 OSW_OK = 0
-OSW_SESSION_ASYNC_ADMIT = 1
 
 
 class osw_dims(C.Structure):
@@ -85,7 +84,7 @@ _SIGS = {
                                        P(osw_decode_opts), P(osw_window_result)]),
     "osw_transcribe_refill": (C.c_int, [C.c_void_p, C.c_void_p, P(C.c_int64), C.c_int32, C.c_int32,
                                         P(osw_decode_opts), P(osw_window_result), C.c_int32]),
-    "osw_session_begin": (C.c_int, [C.c_void_p, P(osw_decode_opts), C.c_int32]),
+    "osw_session_begin": (C.c_int, [C.c_void_p, P(osw_decode_opts)]),
     "osw_session_add": (C.c_int, [C.c_void_p, C.c_void_p, P(C.c_int64), C.c_int32, P(osw_session_window)]),
     "osw_session_step": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, P(osw_window_result), P(C.c_int64), C.c_int32,
                                    P(C.c_int32), P(C.c_int32), P(C.c_int32)]),

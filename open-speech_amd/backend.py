@@ -147,9 +147,7 @@ class HipWhisperBackend:
             tok = WhisperTokenizer(src.dims.n_vocab, src.tokenizer_json)
             runner = BatchRunner(engines, tok, max_wait_ms=wait_ms, gap_ms=gap_ms, split=split,
                                  continuous=continuous, refill_min=int(os.environ.get("STT_HIP_REFILL_MIN", "1")),
-                                 spread_ms=float(spread) if spread else None,
-                                 async_admit=os.environ.get("STT_HIP_SESSION_ASYNC", "0") != "0",
-                                 consolidate_ms=float(os.environ.get("STT_HIP_CONSOLIDATE_MS", "0")))
+                                 spread_ms=float(spread) if spread else None)
             self._models[model_id] = _Model(src, runner, tok, engines)
             now = time.time()
             self._loaded_at[model_id] = now

@@ -667,11 +667,7 @@ void encoder_layer(osw_ctx* c, int i, int nb) {
 }
 
 // slots (row refill): window i's cross K/V goes to decoder row slots[i] of a c->B-row layout
-// side (decode sessions, asynchronous admission): the encoder runs on this stream after the
-// work already on c->stream (side_in), and side_done is recorded at its end; c->stream does
-// NOT wait for it (the session admits the windows once side_done has completed)
-void encode(osw_ctx* c, const osw_window* wins, int n, const int* slots = nullptr, hipStream_t side = nullptr,
-            hipEvent_t side_in = nullptr, hipEvent_t side_done = nullptr) {
+void encode(osw_ctx* c, const osw_window* wins, int n, const int* slots = nullptr) {
     REQUIRE(c->finalized, "weights not finalized");
     REQUIRE(n >= 1 && n <= c->B, "window count out of range");
     const osw_dims& d = c->d;
@@ -715,11 +711,7 @@ void encode(osw_ctx* c, const osw_window* wins, int n, const int* slots = nullpt
     // every CU (OSW_GEMM_GRID=256 in the config-5 simulation: 158.6 -> 164.0 calls/s)
     static const bool share_small = getenv("OSW_SHARE_SMALL") != nullptr;  // A/B switch
     if (n < c->baton_min && !share_small) c->share_cus = false;
-    if (side) {
-        HIPCHK(hipEventRecord(side_in, dec_stream));
-        HIPCHK(hipStreamWaitEvent(side, side_in, 0));
-        c->stream = side;
-    } else if (c->enc_stream) {
+    if (c->enc_stream) {
         HIPCHK(hipEventRecord(c->enc_in, dec_stream));
         HIPCHK(hipStreamWaitEvent(c->enc_stream, c->enc_in, 0));
         c->stream = c->enc_stream;
@@ -764,9 +756,7 @@ void encode(osw_ctx* c, const osw_window* wins, int n, const int* slots = nullpt
         HIPCHK(hipEventRecord(c->baton->ev, c->stream));
         c->baton->recorded = true;
     }
-    if (side) {
-        HIPCHK(hipEventRecord(side_done, side));
-    } else if (c->enc_stream) {
+    if (c->enc_stream) {
         HIPCHK(hipEventRecord(c->enc_out, c->enc_stream));
         HIPCHK(hipStreamWaitEvent(dec_stream, c->enc_out, 0));
     }
@@ -1492,28 +1482,12 @@ struct Session {
     std::deque<SessionWin> queue;
     int active = 0;
     int64_t steps = 0;
-    // asynchronous admission (OSW_SESSION_ASYNC_ADMIT): the next windows' encoder runs on a
-    // side stream while the decoder keeps stepping; their slots are reserved (enc[slot])
-    // and join at the first chunk boundary after the encoder finished
-    bool async = false;
-    hipStream_t es = nullptr;
-    hipEvent_t ev_in = nullptr, ev_done = nullptr;
-    bool enc_pending = false;
-    std::vector<char> enc;
-    std::vector<int> pend_pack;
-    int pend_k = 0;
-    ~Session() {
-        if (ev_done) (void)hipEventSynchronize(ev_done);
-        if (es) (void)hipStreamDestroy(es);
-        if (ev_in) (void)hipEventDestroy(ev_in);
-        if (ev_done) (void)hipEventDestroy(ev_done);
-    }
 };
 
 namespace {
 using osw::SelState;
 
-void session_begin(osw_ctx* c, const osw_decode_opts* o, int flags) {
+void session_begin(osw_ctx* c, const osw_decode_opts* o) {
     REQUIRE(o, "null decode options");
     REQUIRE(!c->sess, "a decode session is already open on this context");
     REQUIRE(!(o->temperature > 0.f), "decode sessions decode at temperature 0 (greedy or beam search)");
@@ -1565,13 +1539,6 @@ void session_begin(osw_ctx* c, const osw_decode_opts* o, int flags) {
     HIPCHK(hipMemsetAsync(c->budget, 0, (size_t)R * 4, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     S->slot_tag.assign(S->W, -1);
-    S->enc.assign(S->W, 0);
-    if (flags & OSW_SESSION_ASYNC_ADMIT) {
-        S->async = true;
-        HIPCHK(hipStreamCreateWithFlags(&S->es, hipStreamNonBlocking));
-        HIPCHK(hipEventCreateWithFlags(&S->ev_in, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&S->ev_done, hipEventDisableTiming));
-    }
     c->row_pos = true;
     c->kv_rows = c->R;
     c->xkv_windows = c->B;
@@ -1607,24 +1574,8 @@ void session_add(osw_ctx* c, const int16_t* pcm, const int64_t* offsets, int n, 
     }
 }
 
-// asynchronous admission: finish the pending encoder's admission once it completed (wait
-// for it only when nothing else decodes, `must`), then start the next queued windows' encoder
-void session_admit(osw_ctx* c, int refill_min, bool must = false) {
+void session_admit(osw_ctx* c, int refill_min) {
     Session* S = c->sess;
-    if (S->async && S->enc_pending) {
-        const hipError_t q = must && S->active == 0 ? hipEventSynchronize(S->ev_done) : hipEventQuery(S->ev_done);
-        if (q == hipErrorNotReady) return;
-        HIPCHK(q);
-        HIPCHK(hipMemcpyAsync(c->refill_pack, S->pend_pack.data(), S->pend_pack.size() * 4, hipMemcpyHostToDevice,
-                              c->stream));
-        launch_session_rows(c->refill_pack, S->pend_k, 3 + S->ctx, S->beam, S->ctx, S->ctx, c->prompt, c->budget,
-                            c->cur_tok, c->pos, c->sel, S->beam > 1 ? c->anc : nullptr,
-                            S->beam > 1 ? c->bwin : nullptr, c->stream);
-        HIPCHK(hipGetLastError());
-        for (int i = 0; i < S->W; ++i) S->enc[i] = 0;
-        S->active += S->pend_k;
-        S->enc_pending = false;
-    }
     std::vector<int> free_slots;
     for (int i = 0; i < S->W; ++i)
         if (S->slot_tag[i] < 0) free_slots.push_back(i);
@@ -1659,18 +1610,6 @@ void session_admit(osw_ctx* c, int refill_min, bool must = false) {
         e[3 + np + 2] = S->o.task_token;
         if (S->o.without_timestamps) e[3 + np + 3] = S->o.no_timestamps;
     }
-    if (S->async) {
-        encode(c, wins.data(), k, slots.data(), S->es, S->ev_in, S->ev_done);
-        for (int i = 0; i < k; ++i) {
-            S->slot_tag[free_slots[i]] = S->queue[i].w.tag;
-            S->enc[free_slots[i]] = 1;
-        }
-        for (int i = 0; i < k; ++i) S->queue.pop_front();
-        S->pend_pack = std::move(pack);
-        S->pend_k = k;
-        S->enc_pending = true;
-        return;
-    }
     encode(c, wins.data(), k, slots.data());
     for (int i = 0; i < k; ++i) S->slot_tag[free_slots[i]] = S->queue[i].w.tag;
     HIPCHK(hipMemcpyAsync(c->refill_pack, pack.data(), pack.size() * 4, hipMemcpyHostToDevice, c->stream));
@@ -1695,13 +1634,13 @@ int session_step(osw_ctx* c, int max_chunks, int refill_min, osw_window_result* 
     }();
     const int beam = S->beam;
     int done = 0;
-    if (max_chunks == 0) {  // admission only: the queued windows' encoder, waited for (async: started)
+    if (max_chunks == 0) {  // admission only: the queued windows' encoder, waited for
         session_admit(c, refill_min);
-        if (!S->async) HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
         return 0;
     }
     for (int chunk = 0; chunk < max_chunks && done == 0; ++chunk) {
-        session_admit(c, refill_min, true);
+        session_admit(c, refill_min);
         if (S->active == 0) break;
         int hi = 0;
         for (int i = 0; i < S->W; ++i)
@@ -1742,7 +1681,7 @@ int session_step(osw_ctx* c, int max_chunks, int refill_min, osw_window_result* 
         HIPCHK(hipStreamSynchronize(c->stream));
         std::vector<int> fin;
         for (int i = 0; i < hi; ++i)
-            if (S->slot_tag[i] >= 0 && !S->enc[i] && (beam > 1 ? bw[i].done : st[i].done)) fin.push_back(i);
+            if (S->slot_tag[i] >= 0 && (beam > 1 ? bw[i].done : st[i].done)) fin.push_back(i);
         if (fin.empty()) continue;
         // the finished windows' tokens: beam -> the best hypothesis per window (btok),
         // greedy -> the row's picks (tokens)
@@ -2084,13 +2023,12 @@ int osw_transcribe_refill(osw_ctx* c, const int16_t* pcm, const int64_t* offsets
     });
 }
 
-int osw_session_begin(osw_ctx* c, const osw_decode_opts* opts, int32_t flags) {
+int osw_session_begin(osw_ctx* c, const osw_decode_opts* opts) {
     return guard([&] {
         REQUIRE(c, "null ctx");
-        REQUIRE((flags & ~OSW_SESSION_ASYNC_ADMIT) == 0, "unknown session flags");
         std::lock_guard<std::mutex> lk(c->mu);
         DeviceScope dev_scope_((c->device));
-        session_begin(c, opts, flags);
+        session_begin(c, opts);
     });
 }
 
@@ -2112,7 +2050,7 @@ int osw_session_step(osw_ctx* c, int32_t max_chunks, int32_t refill_min, osw_win
         LaneCall call_(c);
         *n_done = session_step(c, std::max(0, max_chunks), refill_min, res, tags_out, cap);
         *n_active = c->sess->active;
-        *n_queued = (int32_t)c->sess->queue.size() + (c->sess->enc_pending ? c->sess->pend_k : 0);
+        *n_queued = (int32_t)c->sess->queue.size();
         resolve_events(c);
     });
 }

@@ -233,17 +233,6 @@ class _SessionLane(_Worker):
                         continue
                     if idle:
                         head = dq.items[0]
-                        if pool.consolidate_ms and session_supported(head.opts):
-                            # a sibling's open session of this key has room: leave the request
-                            # to it (it admits at its next chunk boundary) unless it waited
-                            # consolidate_ms -- one session of many windows amortises each
-                            # decoder step over more rows
-                            left = head.t_enq + pool.consolidate_ms / 1000.0 - time.monotonic()
-                            hk = head.opts.key()
-                            if left > 0 and any(w is not self and w.alive and getattr(w, "key", None) == hk
-                                                and 0 < w.inflight < w.engine.max_batch for w in dq.lanes):
-                                dq.cv.wait(timeout=left)
-                                continue
                         if not session_supported(head.opts):
                             k = head.opts.key()
                             batch = [r for r in dq.items if r.opts.key() == k][:self.engine.max_batch]
@@ -308,7 +297,6 @@ class _SessionLane(_Worker):
             if idle and is_open:
                 eng.session_end()
                 is_open = False
-                self.key = None
             got = self._admit(key, eng.max_batch - len(flights), idle)
             if got is None:
                 break
@@ -323,10 +311,8 @@ class _SessionLane(_Worker):
                     continue
                 _, k, reqs = got
                 if reqs and not is_open:
-                    eng.session_begin(session_config(reqs[0].opts, pool.suppress_for(reqs[0].opts)),
-                                      async_admit=pool.async_admit)
+                    eng.session_begin(session_config(reqs[0].opts, pool.suppress_for(reqs[0].opts)))
                     key, is_open = k, True
-                    self.key = key
                 for r in reqs:
                     tag += 1
                     flights[tag] = [r, clip_state(0, r.pcm, r.opts, tok), None]
@@ -338,7 +324,7 @@ class _SessionLane(_Worker):
                         answer(tag, e)
                 if not flights:
                     continue
-                if added and not pool.async_admit:
+                if added:
                     # admission on its own (the encoder, waited for), counted on the GPU's
                     # queue so that the other lanes take turns with it
                     added = False
@@ -402,8 +388,7 @@ class _SessionLane(_Worker):
 class BatchRunner:
     def __init__(self, engines: list, tokenizer: WhisperTokenizer, max_wait_ms: float = 5.0,
                  gap_ms: float | None = None, split: bool = True, max_pace_ms: float = 100.0,
-                 continuous: bool = False, refill_min: int = 1, spread_ms: float | None = None,
-                 async_admit: bool = False, consolidate_ms: float = 0.0):
+                 continuous: bool = False, refill_min: int = 1, spread_ms: float | None = None):
         self.tokenizer = tokenizer
         self.max_wait_ms = max_wait_ms
         self.gap_ms = gap_ms
@@ -412,8 +397,6 @@ class BatchRunner:
         self.continuous = continuous
         self.refill_min = refill_min
         self.spread_ms = spread_ms
-        self.async_admit = async_admit        # sessions encode queued windows beside the decoder
-        self.consolidate_ms = consolidate_ms  # idle lanes leave requests to an open session with room
         self._sup_cache: dict = {}
         self._lock = threading.Lock()
         self.queues: list[_DevQueue] = []

@@ -58,7 +58,7 @@ class FakeEngine:
         return outs
 
     # decode sessions (runner._SessionLane): a window finishes 1-3 steps after admission
-    def session_begin(self, cfg, async_admit=False):
+    def session_begin(self, cfg):
         assert getattr(self, "_sess", None) is None
         self._sess = dict(cfg=cfg, q=[], active=[])
         self.sessions = getattr(self, "sessions", 0) + 1
@@ -677,7 +677,7 @@ def test_session_lane_error_before_flight_fails_taken_requests():
     from open_speech_amd.tokenizer import WhisperTokenizer
 
     class Eng(FakeEngine):
-        def session_begin(self, cfg, async_admit=False):
+        def session_begin(self, cfg):
             raise ValueError("cannot open")
 
     runner = BatchRunner([Eng(D.MICRO_TEST, 0, 4)], WhisperTokenizer(51866), continuous=True)

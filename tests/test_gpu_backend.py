@@ -277,8 +277,7 @@ def test_backend_default_config_matches_oracle_seek_loop(monkeypatch, tmp_path):
     assert sum(1 for e in engines if e._wins) >= 2
 
 
-@pytest.mark.parametrize("async_admit", [False, True])
-def test_backend_continuous_matches_oracle_seek_loop(monkeypatch, tmp_path, async_admit):
+def test_backend_continuous_matches_oracle_seek_loop(monkeypatch, tmp_path):
     """Continuous batching as deployed (the default, STT_HIP_CONTINUOUS=1, runner._SessionLane):
     the backend's defaults (beam 5, 3 lanes, max batch 16), four concurrent requests
     (75, 61, 47 and 12 s WAVs) arriving while earlier ones decode, so windows of different
@@ -305,7 +304,6 @@ def test_backend_continuous_matches_oracle_seek_loop(monkeypatch, tmp_path, asyn
         monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("STT_HIP_GPUS", "0")
     monkeypatch.setenv("STT_HIP_CONTINUOUS", "1")
-    monkeypatch.setenv("STT_HIP_SESSION_ASYNC", "1" if async_admit else "0")
 
     added, done, shared = {}, {}, []
     lock = threading.Lock()
@@ -321,9 +319,9 @@ def test_backend_continuous_matches_oracle_seek_loop(monkeypatch, tmp_path, asyn
         def sibling(self, max_batch=None):
             return Recorder(self.eng.sibling(max_batch))
 
-        def session_begin(self, cfg, async_admit=False):
+        def session_begin(self, cfg):
             assert cfg.beam_size == 5, "the backend's default decoding is beam search width 5"
-            return self.eng.session_begin(cfg, async_admit=async_admit)
+            return self.eng.session_begin(cfg)
 
         def session_add(self, wins):
             with lock:

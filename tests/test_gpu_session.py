@@ -45,9 +45,9 @@ def _alone(eng, w, cfg):
     return eng.decode(2, c, prefix=[w["prefix"]] * 2 if w["prefix"] else None, languages=[w["language_token"]] * 2)[0]
 
 
-def _run_session(eng, cfg, wins, add_in=(1.0,), refill_min=1, async_admit=False):
+def _run_session(eng, cfg, wins, add_in=(1.0,), refill_min=1):
     """Add the windows in portions (fractions of the list) between steps; collect results."""
-    eng.session_begin(cfg, async_admit=async_admit)
+    eng.session_begin(cfg)
     got = {}
     try:
         cut = [0] + [int(round(f * len(wins))) for f in add_in]
@@ -84,9 +84,8 @@ def _compare(eng, cfg, wins, got):
         assert g.language == r.language, w["tag"]
 
 
-@pytest.mark.parametrize("async_admit", [False, True])
 @pytest.mark.parametrize("beam", [1, 5])
-def test_session_matches_alone_tiny(beam, async_admit):
+def test_session_matches_alone_tiny(beam):
     """17 windows (3 clip lengths, seeks into a 47 s clip, prefixes, detected and fixed
     languages, budgets 4..22 tokens) through 6 slots, added in three portions while
     earlier ones decode."""
@@ -97,7 +96,7 @@ def test_session_matches_alone_tiny(beam, async_admit):
         sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
         cfg = DecodeConfig(suppress_tokens=sup, max_length=64, beam_size=beam)
         wins = _windows(d, 17, 200)
-        got = _run_session(eng, cfg, wins, add_in=(0.3, 0.6, 1.0), async_admit=async_admit)
+        got = _run_session(eng, cfg, wins, add_in=(0.3, 0.6, 1.0))
         _compare(eng, cfg, wins, got)
         assert len({len(g.tokens) for g in got.values()}) > 3
     finally:
@@ -115,15 +114,14 @@ def test_session_no_budget_without_timestamps():
         wins = _windows(d, 9, 300)
         for w in wins:
             w["token_budget"] = 0
-        got = _run_session(eng, cfg, wins, refill_min=3, async_admit=True)
+        got = _run_session(eng, cfg, wins, refill_min=3)
         _compare(eng, cfg, wins, got)
     finally:
         eng.close()
 
 
-@pytest.mark.parametrize("async_admit", [False, True])
 @pytest.mark.parametrize("beam", [1, 5])
-def test_session_matches_alone_turbo(beam, async_admit):
+def test_session_matches_alone_turbo(beam):
     """large-v3-turbo dims (random weights): 10 windows through 4 slots."""
     d = D.LARGE_V3_TURBO
     eng = WhisperEngine(d, device=0, max_batch=4)
@@ -132,7 +130,7 @@ def test_session_matches_alone_turbo(beam, async_admit):
         sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
         cfg = DecodeConfig(suppress_tokens=sup, max_length=48, beam_size=beam)
         wins = _windows(d, 10, 400)
-        got = _run_session(eng, cfg, wins, add_in=(0.5, 1.0), async_admit=async_admit)
+        got = _run_session(eng, cfg, wins, add_in=(0.5, 1.0))
         _compare(eng, cfg, wins, got)
     finally:
         eng.close()

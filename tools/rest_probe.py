@@ -53,7 +53,7 @@ for t in ts:
     t.join()
 wall = time.perf_counter() - t0
 gap = os.environ.get("STT_HIP_BATCH_GAP_MS", "1 (default)")
-mode = "continuous" if os.environ.get("STT_HIP_CONTINUOUS", "0") != "0" else "batch"
+mode = "continuous" if os.environ.get("STT_HIP_CONTINUOUS", "1") != "0" else "batch"
 print(f"{mode}{' mix' if MIX else ''} audio {sum(LENS[(i + k) % 8] for i in range(C) for k in range(R)) / wall:.0f} s/s, "
       f"gap_ms {gap}: {C} callers x {R} calls, jitter {J:.0f} ms: {len(lat) / wall:.2f} calls/s, "
       f"latency p50 {np.median(lat):.0f} ms p95 {np.percentile(lat, 95):.0f} ms", flush=True)

@@ -67,6 +67,9 @@ def parse(argv=None):
     ap.add_argument("--stream-sessions", type=int, default=32,
                     help="BASELINE configs[4]: concurrent /v1/audio/stream sessions simulated through the backend "
                          "(0 = skip)")
+    ap.add_argument("--rest-callers", type=int, default=16,
+                    help="mixed-length REST load, continuous vs batch-at-a-time (0: skip)")
+    ap.add_argument("--rest-calls", type=int, default=8, help="calls per REST caller")
     ap.add_argument("--stream-speech-s", type=float, default=6.0, help="seconds of speech per streaming session")
     ap.add_argument("--refill-min", type=int, default=REFILL_MIN,
                     help="row refill (realistic lengths): admit queued clips once this many rows are free")
@@ -175,6 +178,58 @@ def cpu_baseline(dims, n_tokens_per_clip: float, decode_steps: int) -> dict:
     return {"value": round(30.0 / per_clip, 4), "unit": "audio-sec/sec", "cores": int(cores), "kind": "port",
             "sample": f"oracle (numpy fp32) on 1 x 30 s clip: log-mel {t1 - t0:.2f}s + encoder+crossKV "
                       f"{t2 - t1:.2f}s + {how}"}
+
+
+def rest_mixed(callers: int, calls: int, model: str = "random:large-v3-turbo") -> dict:
+    """Mixed-length REST load on the drop-in backend (tools/rest_probe.py ... mix): `callers`
+    threads each post `calls` WAVs of 4-75 s (1-3 windows) through transcribe() with
+    exponentially distributed think time (mean 40 ms), once with continuous batching (the
+    default, runner._SessionLane) and once batch at a time (STT_HIP_CONTINUOUS=0), so the
+    line shows what continuous batching buys on the load it is for (src/main.py:305 calls
+    transcribe() from the default executor).  Beam 5, 4 tokens/s length control."""
+    import threading
+
+    from open_speech_amd.audio import pcm_to_wav
+    from open_speech_amd.backend import HipWhisperBackend
+
+    os.environ.setdefault("STT_HIP_TOKENS_PER_SEC", "4")
+    lens = (4.0, 12.0, 30.0, 45.0, 75.0, 20.0, 8.0, 60.0)
+    wavs = [pcm_to_wav(synth.chirp_clip(800 + i, x).tobytes(), 16000) for i, x in enumerate(lens)]
+    out = {"callers": callers, "calls_per_caller": calls, "clip_s": list(lens), "think_ms_mean": 40}
+    prev = os.environ.get("STT_HIP_CONTINUOUS")
+    for mode, flag in (("continuous", "1"), ("batch_at_a_time", "0")):
+        os.environ["STT_HIP_CONTINUOUS"] = flag
+        be = HipWhisperBackend()
+        be.load_model(model)
+        be.transcribe(audio=wavs[0], model=model, language=None, response_format="json")   # warm
+        lat, lock = [], threading.Lock()
+
+        def caller(i):
+            rng = np.random.default_rng(i)
+            for k in range(calls):
+                time.sleep(rng.exponential(0.040))
+                t = time.perf_counter()
+                be.transcribe(audio=wavs[(i + k) % len(wavs)], model=model, language=None, response_format="json")
+                with lock:
+                    lat.append(time.perf_counter() - t)
+
+        ts = [threading.Thread(target=caller, args=(i,)) for i in range(callers)]
+        t0 = time.perf_counter()
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        wall = time.perf_counter() - t0
+        be.unload_model(model)
+        audio = sum(lens[(i + k) % len(lens)] for i in range(callers) for k in range(calls))
+        out[mode] = {"calls_per_s": round(len(lat) / wall, 2), "audio_sec_per_sec": round(audio / wall, 1),
+                     "latency_p50_ms": round(1e3 * float(np.median(lat)), 1),
+                     "latency_p95_ms": round(1e3 * float(np.percentile(lat, 95)), 1)}
+    if prev is None:
+        os.environ.pop("STT_HIP_CONTINUOUS", None)
+    else:
+        os.environ["STT_HIP_CONTINUOUS"] = prev
+    return out
 
 
 def stream_sessions(n_sessions: int, speech_s: float, model: str = "random:large-v3-turbo", backend=None,
@@ -533,6 +588,10 @@ def main(argv=None):
         if a.stream_sessions > 0 and world == 1:
             stream = stream_sessions(a.stream_sessions, a.stream_speech_s)
 
+        rest = None
+        if a.rest_callers > 0 and world == 1:
+            rest = rest_mixed(a.rest_callers, a.rest_calls)
+
         ingest_t = None
         if world == 1:
             ingest_t = ingest_timing(device=dev.index)
@@ -556,6 +615,7 @@ def main(argv=None):
             "beam5": beam5_lanes,
             "realistic_lengths": realistic,
             "streaming": stream,
+            "rest_mixed": rest,
             "ingest": ingest_t,
             "beam5_audio_sec_per_sec_1lane": beam5,
             "realtime_factor": round(value, 1),

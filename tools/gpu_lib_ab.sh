@@ -3,7 +3,7 @@
 set -e
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/$1; shift; mkdir -p $O
-ARGS=${BENCH_ARGS:-"--steps 3 --latency-repeats 0 --beam5 1 --beam5-steps 4 --beam5-latency-repeats 10 --realistic-steps 0 --stream-sessions 0 --no-cpu-baseline"}
+ARGS=${BENCH_ARGS:-"--steps 3 --latency-repeats 0 --beam5 1 --beam5-steps 4 --beam5-latency-repeats 10 --realistic-steps 0 --stream-sessions 0 --rest-callers 0 --no-cpu-baseline"}
 if [ -n "$PRE_TESTS" ]; then
   timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "$PRE_TESTS" > $O/gpu_tests.log 2>&1
   tail -1 $O/gpu_tests.log

@@ -21,7 +21,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 TAG=$1; shift
 O=gpurun_out/$TAG; mkdir -p $O
 export TMPDIR=/tmp
-QUICK="--latency-repeats 0 --beam5-latency-repeats 0 --beam5 0 --beam5-steps 0 --realistic-steps 0 --stream-sessions 0 --no-cpu-baseline"
+QUICK="--latency-repeats 0 --beam5-latency-repeats 0 --beam5 0 --beam5-steps 0 --realistic-steps 0 --stream-sessions 0 --rest-callers 0 --no-cpu-baseline"
 i=0
 for s in "$@"; do
   i=$((i+1))
@@ -60,7 +60,7 @@ for s in "$@"; do
       [ $rc -eq 0 ] && python3 tools/trace_classes.py $O/sprof_$i/run_kernel_trace.csv $O/stream_classes_$i.txt && head -16 $O/stream_classes_$i.txt
       rm -f $O/sprof_$i/run_kernel_trace.csv ;;
     b1)
-      timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/b1prof -o run -- python3 bench.py --steps 1 --warmup 0 --lanes 1 --latency-repeats 4 --latency-warmup 1 --beam5-latency-repeats 0 --beam5 0 --beam5-steps 0 --realistic-steps 0 --stream-sessions 0 --no-cpu-baseline > $O/b1.json 2> $O/b1.err
+      timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/b1prof -o run -- python3 bench.py --steps 1 --warmup 0 --lanes 1 --latency-repeats 4 --latency-warmup 1 --beam5-latency-repeats 0 --beam5 0 --beam5-steps 0 --realistic-steps 0 --stream-sessions 0 --rest-callers 0 --no-cpu-baseline > $O/b1.json 2> $O/b1.err
       rc=$?; [ $rc -eq 0 ] && python3 tools/b1_breakdown.py $O/b1prof/run_kernel_trace.csv $((5*445)) > $O/b1_breakdown.txt && head -30 $O/b1_breakdown.txt
       rm -f $O/b1prof/run_kernel_trace.csv ;;
     repro)

@@ -11,6 +11,7 @@
 #   stream      config-5 simulation with host breakdown     -> $O/stream.json
 #   streamprof  the same under a kernel trace, eager decode -> $O/stream_classes.txt
 #   b1          batch-1 greedy step breakdown               -> $O/b1_breakdown.txt
+#   b1beam      batch-1 beam-5 step breakdown               -> $O/b1beam_breakdown.txt
 #   repro       tools/graph_prof_repro (mode 2) under a rocprofv3 kernel trace -> $O/repro.log
 #   bench:ARGS  bench.py with extra args (commas -> spaces) -> $O/bench_N.json
 #   py:SCRIPT,ARGS  python3 SCRIPT ARGS                     -> $O/py_N.txt
@@ -63,6 +64,10 @@ for s in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/b1prof -o run -- python3 bench.py --steps 1 --warmup 0 --lanes 1 --latency-repeats 4 --latency-warmup 1 --beam5-latency-repeats 0 --beam5 0 --beam5-steps 0 --realistic-steps 0 --stream-sessions 0 --rest-callers 0 --no-cpu-baseline > $O/b1.json 2> $O/b1.err
       rc=$?; [ $rc -eq 0 ] && python3 tools/b1_breakdown.py $O/b1prof/run_kernel_trace.csv $((5*445)) > $O/b1_breakdown.txt && head -30 $O/b1_breakdown.txt
       rm -f $O/b1prof/run_kernel_trace.csv ;;
+    b1beam)
+      timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/b1bprof -o run -- python3 bench.py --steps 1 --warmup 0 --lanes 1 --latency-repeats 0 --beam5-latency-repeats 4 --latency-warmup 1 --beam5 0 --beam5-steps 0 --realistic-steps 0 --stream-sessions 0 --rest-callers 0 --no-cpu-baseline > $O/b1beam.json 2> $O/b1beam.err
+      rc=$?; [ $rc -eq 0 ] && python3 tools/b1_breakdown.py $O/b1bprof/run_kernel_trace.csv $((5*445)) > $O/b1beam_breakdown.txt && head -40 $O/b1beam_breakdown.txt
+      rm -f $O/b1bprof/run_kernel_trace.csv ;;
     repro)
       timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/repro -o run -- ./tools/graph_prof_repro 3 300 2 > $O/repro.log 2>&1
       rc=$?; tail -3 $O/repro.log; rm -f $O/repro/run_kernel_trace.csv ;;

@@ -690,3 +690,36 @@ def test_session_lane_error_before_flight_fails_taken_requests():
                 r.fut.result(timeout=10)
     finally:
         runner.close()
+
+
+def test_session_lane_switches_keys():
+    """Requests of two decode configurations on one lane: the lane's session takes its own
+    key's requests, stops admitting once a request of the other key waited max_pace_ms,
+    drains and opens a session for the other key; every request is answered."""
+    from concurrent.futures import Future
+    from open_speech_amd.runner import BatchRunner, _Req
+    from open_speech_amd.segments import TranscribeOptions
+    from open_speech_amd.tokenizer import WhisperTokenizer
+
+    class Eng(FakeEngine):
+        def __init__(self):
+            super().__init__(D.MICRO_TEST, 0, 4)
+            self.cfgs = []
+            self.step_sleep = 0.002
+
+        def session_begin(self, cfg):
+            self.cfgs.append(cfg.beam_size)
+            return super().session_begin(cfg)
+
+    e = Eng()
+    runner = BatchRunner([e], WhisperTokenizer(51866), continuous=True, max_pace_ms=20)
+    try:
+        reqs = [_Req(synth.chirp_clip(i, 3.0), TranscribeOptions(language="en", beam_size=5 if i % 2 else 1), Future())
+                for i in range(12)]
+        for r in reqs:
+            runner.submit_req(r)
+        for r in reqs:
+            assert r.fut.result(timeout=30).segments
+        assert set(e.cfgs) == {1, 5} and len(e.cfgs) >= 2
+    finally:
+        runner.close()

@@ -1052,21 +1052,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void s
 // The KV cache is never copied: row r's key at position p lives in the slot of row
 // anc[r][p] (written at step p); the reorder copies only anc / tokens / state.
 
-// block-wide argmax (value desc, index asc) of one candidate per thread, 256 threads
-__device__ __forceinline__ ArgMax block_amax(ArgMax a, ArgMax* red) {
-    auto step = [&](auto o) {
-        constexpr int O = decltype(o)::value;
-        a = amax(a, ArgMax{xor_lane<O>(a.v), xor_lane<O>(a.i)});
-    };
-    step(IC<32>{}), step(IC<16>{}), step(IC<8>{}), step(IC<4>{}), step(IC<2>{}), step(IC<1>{});
-    const int w = threadIdx.x >> 6;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[w] = a;
-    __syncthreads();
-    ArgMax r = red[0];
-    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) r = amax(r, red[i]);
-    return r;
-}
 
 // grid windows, 256 threads: merge the candidates, register finished hypotheses,
 // pick the surviving beams and reorder their tokens / ancestry / state.
@@ -1083,7 +1068,7 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
     __shared__ float cs[MAXC];
     __shared__ int ci[MAXC];
     __shared__ BeamCand top[2 * KM];
-    __shared__ ArgMax red[4];
+    __shared__ ArgMax wtop[4][2 * KM];
     __shared__ int lseq[KM][448];
     __shared__ int lanc[KM][448];
     __shared__ SelState lst[KM];
@@ -1161,19 +1146,69 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
     }
     if (tid < K) lst[tid] = st[r0 + tid];
     __syncthreads();
-    for (int r = 0; r < K2; ++r) {
-        ArgMax a{-INFINITY, INT_MAX};
-        int at = -1;
-        for (int i = tid; i < nc; i += 256) {
-            const ArgMax b{cs[i], ci[i]};
-            if (b.i != INT_MAX && !(b.v != b.v)) {
-                const ArgMax m = amax(a, b);
-                if (m.i != a.i || m.v != a.v) { a = m; at = i; }
+    {
+        // the top K2 candidates by (score desc, flat id asc), NaN scores and INT_MAX ids
+        // excluded, {-inf, INT_MAX} past the last valid one.  Each wave pops its own top K2
+        // from registers (wave argmax, no barrier; flat ids are unique, so one lane owns
+        // each pop), then wave 0 ranks the 4*K2 survivors: the global top K2 lie among
+        // them, so this is the list (and order) of K2 block-wide pops, with one barrier
+        // instead of 2*K2.
+        constexpr int CPT = (MAXC + 255) / 256;
+        const int lane = tid & 63, wv = tid >> 6;
+        float cv[CPT];
+        int cx[CPT];
+        unsigned live = 0;
+#pragma unroll
+        for (int j = 0; j < CPT; ++j) {
+            const int i = tid + 256 * j;
+            cv[j] = -INFINITY;
+            cx[j] = INT_MAX;
+            if (i < nc) {
+                cv[j] = cs[i];
+                cx[j] = ci[i];
+                if (cx[j] != INT_MAX && !(cv[j] != cv[j])) live |= 1u << j;
             }
         }
-        const ArgMax g = block_amax(a, red);
-        if (a.i == g.i && at >= 0 && g.i != INT_MAX) cs[at] = __builtin_nanf("");  // unique flat ids: one owner
-        if (tid == 0) top[r] = BeamCand{g.v, g.i};
+        int at = -1;
+        auto mine = [&]() {
+            ArgMax a{-INFINITY, INT_MAX};
+            at = -1;
+#pragma unroll
+            for (int j = 0; j < CPT; ++j)
+                if ((live >> j) & 1u) {
+                    const ArgMax m = amax(a, ArgMax{cv[j], cx[j]});
+                    if (m.i != a.i || m.v != a.v) { a = m; at = j; }
+                }
+            return a;
+        };
+        ArgMax my = mine();
+        for (int r = 0; r < K2; ++r) {
+            ArgMax a = my;
+            auto stp = [&](auto o) {
+                constexpr int O = decltype(o)::value;
+                a = amax(a, ArgMax{xor_lane<O>(a.v), xor_lane<O>(a.i)});
+            };
+            stp(IC<32>{}), stp(IC<16>{}), stp(IC<8>{}), stp(IC<4>{}), stp(IC<2>{}), stp(IC<1>{});
+            if (lane == 0) wtop[wv][r] = a;
+            if (a.i != INT_MAX && at >= 0 && my.i == a.i) {
+                live &= ~(1u << at);
+                my = mine();
+            }
+        }
+        __syncthreads();
+        if (wv == 0) {
+            const int S = 4 * K2;  // <= 64 (K2 <= 2 * KM <= 16)
+            const ArgMax e = lane < S ? wtop[lane / K2][lane % K2] : ArgMax{-INFINITY, INT_MAX};
+            const bool valid = lane < S && e.i != INT_MAX;
+            int rank = 0;
+            for (int j = 0; j < S; ++j) {
+                const ArgMax f = wtop[j / K2][j % K2];
+                rank += (f.i != INT_MAX && (f.v > e.v || (f.v == e.v && f.i < e.i))) ? 1 : 0;
+            }
+            const int nvalid = __popcll(__ballot(valid));
+            if (valid && rank < K2) top[rank] = BeamCand{e.v, e.i};
+            if (lane < K2 && lane >= nvalid) top[lane] = BeamCand{-INFINITY, INT_MAX};
+        }
         __syncthreads();
     }
     if (tid == 0) {

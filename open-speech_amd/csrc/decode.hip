@@ -1065,86 +1065,81 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
                                                           int* __restrict__ best_tok, int* __restrict__ cur_tok,
                                                           int max_tokens) {
     constexpr int MAXC = KM * BEAM_SLICES * 2 * KM;
-    __shared__ float cs[MAXC];
-    __shared__ int ci[MAXC];
+    constexpr int CPT = (MAXC + 255) / 256;      // candidates per thread
+    constexpr int HPT = (KM * 448 + 255) / 256;  // history / ancestry entries per thread
     __shared__ BeamCand top[2 * KM];
     __shared__ ArgMax wtop[4][2 * KM];
     __shared__ int lseq[KM][448];
     __shared__ int lanc[KM][448];
     __shared__ SelState lst[KM];
+    __shared__ SelPart lparts[KM * SEL_SPLIT];
     __shared__ int choose[KM], fin, best_src, best_extra, improved;
     const int w = blockIdx.x, tid = threadIdx.x, K = P.beam, K2 = 2 * K;
     const int r0 = w * K;
     const int step = pos_ptr[P.pos_row ? r0 : 0];
-    if (sel_mode(P, step, st[r0]) != SEL_SAMPLE) return;
+    const SelState s0 = st[r0];
+    if (sel_mode(P, step, s0) != SEL_SAMPLE) return;
     const int nc = K * BEAM_SLICES * K2;
-    const int n = st[r0].n_sampled;  // identical for every row of the window
-    // candidates, token histories and ancestry into LDS: 8 loads per thread per round trip
-    // (clamped addresses), stored once they land (a load-then-store loop is one trip each)
-    constexpr int LB = 8;
+    const int n = s0.n_sampled;  // identical for every row of the window
+    const int plen = row_plen(P, s0);
+    const bool first = step == plen - 1;  // only the prompt hypothesis expands
+    // Every load of the update is issued before any is used (one memory round trip instead of
+    // one per phase): both candidate lists of every (row, slice) (the row's timestamp rule,
+    // known only once its 16 slice statistics are combined, picks one), the slice
+    // statistics, the rows' states, token histories and ancestry.  Clamped addresses.
+    BeamCand ca[CPT], cb[CPT];
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+        const int i = min(tid + 256 * j, nc - 1), k = i / (BEAM_SLICES * K2), sl = (i / K2) % BEAM_SLICES;
+        const BeamCand* src = cand + (((int64_t)(r0 + k) * BEAM_SLICES + sl) * 2) * MAXK2 + i % K2;
+        ca[j] = src[0];
+        cb[j] = src[MAXK2];
+    }
+    SelPart mp{};
+    if (tid < K * SEL_SPLIT) mp = parts[(int64_t)r0 * SEL_SPLIT + tid];
+    SelState ms{};
+    if (tid < K) ms = st[r0 + tid];
+    const int nn = max(n, 1), ns = K * nn, na = K * step;
+    int hv[HPT], av[HPT];
+#pragma unroll
+    for (int j = 0; j < HPT; ++j) {
+        const int i = tid + 256 * j;
+        const int is = min(i, ns - 1), ia = min(i, max(na, 1) - 1);
+        hv[j] = seq[(int64_t)(r0 + is / nn) * max_tokens + min(is % nn, max_tokens - 1)];
+        av[j] = anc[(int64_t)(r0 + ia / max(step, 1)) * ctx + ia % max(step, 1)];
+    }
+    if (tid < K * SEL_SPLIT) lparts[tid] = mp;
+    if (tid < K) lst[tid] = ms;
+#pragma unroll
+    for (int j = 0; j < HPT; ++j) {
+        const int i = tid + 256 * j;
+        if (i < ns && i % nn < n) lseq[i / nn][i % nn] = hv[j];
+        if (i < na) lanc[i / step][i % step] = av[j];
+    }
+    __syncthreads();
     // per row: lse over the allowed tokens, over the allowed timestamps, and the
-    // timestamp-mass rule (the row's 16 slice statistics in fixed order)
+    // timestamp-mass rule (the row's 16 slice statistics merged in fixed order, as
+    // combine_parts does)
     __shared__ float rlse[KM], rsum[KM];
     __shared__ int rts[KM];
     if (tid < K) {
-        rsum[tid] = st[r0 + tid].sum_lp;
-        const SelPart r = combine_parts<false>(parts + (int64_t)(r0 + tid) * SEL_SPLIT);
+        rsum[tid] = lst[tid].sum_lp;
+        SelPart r = lparts[tid * SEL_SPLIT];
+        for (int i = 1; i < SEL_SPLIT; ++i) {
+            const SelPart q = lparts[tid * SEL_SPLIT + i];
+            lse_merge(r.m_all, r.s_all, q.m_all, q.s_all);
+            lse_merge(r.m_ts, r.s_ts, q.m_ts, q.s_ts);
+            ArgMax A = amax(ArgMax{r.v_all, r.i_all}, ArgMax{q.v_all, q.i_all});
+            ArgMax X = amax(ArgMax{r.v_text, r.i_text}, ArgMax{q.v_text, q.i_text});
+            ArgMax T = amax(ArgMax{r.v_ts, r.i_ts}, ArgMax{q.v_ts, q.i_ts});
+            r.v_all = A.v; r.i_all = A.i; r.v_text = X.v; r.i_text = X.i; r.v_ts = T.v; r.i_ts = T.i;
+        }
         const float lse_all = r.m_all + logf(r.s_all);
         const float lse_ts = r.m_ts == -INFINITY ? -INFINITY : r.m_ts + logf(r.s_ts);
         const bool ts_wins = P.with_ts && lse_ts - lse_all > r.v_text - lse_all;
         rlse[tid] = ts_wins ? lse_ts : lse_all;
         rts[tid] = ts_wins;
     }
-    __syncthreads();
-    // candidate (row k, slice, j): list B if the row's timestamps win, else list A; score =
-    // sum_lp + (x - lse) as the per-row log-prob + cumulative score of the reference
-    const int plen = row_plen(P, st[r0]);
-    const bool first = step == plen - 1;  // only the prompt hypothesis expands
-    for (int i0 = tid; i0 < nc; i0 += 256 * LB) {
-        BeamCand c[LB];
-#pragma unroll
-        for (int j = 0; j < LB; ++j) {
-            const int i = min(i0 + 256 * j, nc - 1), k = i / (BEAM_SLICES * K2), sl = (i / K2) % BEAM_SLICES;
-            c[j] = cand[(((int64_t)(r0 + k) * BEAM_SLICES + sl) * 2 + rts[k]) * MAXK2 + i % K2];
-        }
-#pragma unroll
-        for (int j = 0; j < LB; ++j) {
-            const int i = i0 + 256 * j, k = i / (BEAM_SLICES * K2);
-            if (i >= nc) break;
-            const bool none = c[j].i == INT_MAX || (first && k != 0);
-            cs[i] = none ? -INFINITY : rsum[k] + (c[j].s - rlse[k]);
-            ci[i] = none ? INT_MAX : k * P.V + c[j].i;
-        }
-    }
-    const int nn = max(n, 1), ns = K * nn;
-    for (int i0 = tid; i0 < ns; i0 += 256 * LB) {
-        int v[LB];
-#pragma unroll
-        for (int j = 0; j < LB; ++j) {
-            const int i = min(i0 + 256 * j, ns - 1), k = i / nn, jj = min(i % nn, max_tokens - 1);
-            v[j] = seq[(int64_t)(r0 + k) * max_tokens + jj];
-        }
-#pragma unroll
-        for (int j = 0; j < LB; ++j) {
-            const int i = i0 + 256 * j, k = i / nn, jj = i % nn;
-            if (i < ns && jj < n) lseq[k][jj] = v[j];
-        }
-    }
-    const int na = K * step;
-    for (int i0 = tid; i0 < na; i0 += 256 * LB) {
-        int v[LB];
-#pragma unroll
-        for (int j = 0; j < LB; ++j) {
-            const int i = min(i0 + 256 * j, na - 1);
-            v[j] = anc[(int64_t)(r0 + i / step) * ctx + i % step];
-        }
-#pragma unroll
-        for (int j = 0; j < LB; ++j) {
-            const int i = i0 + 256 * j;
-            if (i < na) lanc[i / step][i % step] = v[j];
-        }
-    }
-    if (tid < K) lst[tid] = st[r0 + tid];
     __syncthreads();
     {
         // the top K2 candidates by (score desc, flat id asc), NaN scores and INT_MAX ids
@@ -1153,8 +1148,9 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
         // each pop), then wave 0 ranks the 4*K2 survivors: the global top K2 lie among
         // them, so this is the list (and order) of K2 block-wide pops, with one barrier
         // instead of 2*K2.
-        constexpr int CPT = (MAXC + 255) / 256;
         const int lane = tid & 63, wv = tid >> 6;
+        // candidate (row k, slice, j): list B if the row's timestamps win, else list A; score =
+        // sum_lp + (x - lse) as the per-row log-prob + cumulative score of the reference
         float cv[CPT];
         int cx[CPT];
         unsigned live = 0;
@@ -1164,8 +1160,11 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
             cv[j] = -INFINITY;
             cx[j] = INT_MAX;
             if (i < nc) {
-                cv[j] = cs[i];
-                cx[j] = ci[i];
+                const int k = i / (BEAM_SLICES * K2);
+                const BeamCand c = rts[k] ? cb[j] : ca[j];
+                const bool none = c.i == INT_MAX || (first && k != 0);
+                cv[j] = none ? -INFINITY : rsum[k] + (c.s - rlse[k]);
+                cx[j] = none ? INT_MAX : k * P.V + c.i;
                 if (cx[j] != INT_MAX && !(cv[j] != cv[j])) live |= 1u << j;
             }
         }

@@ -12,6 +12,7 @@
 #   streamprof  the same under a kernel trace, eager decode -> $O/stream_classes.txt
 #   b1          batch-1 greedy step breakdown               -> $O/b1_breakdown.txt
 #   b1beam      batch-1 beam-5 step breakdown               -> $O/b1beam_breakdown.txt
+#   pmcb1beam   SQ counter passes over a batch-1 beam-5 call -> $O/pmc_b1beam_{1,2}.txt
 #   repro       tools/graph_prof_repro (mode 2) under a rocprofv3 kernel trace -> $O/repro.log
 #   bench:ARGS  bench.py with extra args (commas -> spaces) -> $O/bench_N.json
 #   py:SCRIPT,ARGS  python3 SCRIPT ARGS                     -> $O/py_N.txt
@@ -68,6 +69,14 @@ for s in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/b1bprof -o run -- python3 bench.py --steps 1 --warmup 0 --lanes 1 --latency-repeats 0 --beam5-latency-repeats 4 --latency-warmup 1 --beam5 0 --beam5-steps 0 --realistic-steps 0 --stream-sessions 0 --rest-callers 0 --no-cpu-baseline > $O/b1beam.json 2> $O/b1beam.err
       rc=$?; [ $rc -eq 0 ] && python3 tools/b1_breakdown.py $O/b1bprof/run_kernel_trace.csv $((5*445)) > $O/b1beam_breakdown.txt && head -40 $O/b1beam_breakdown.txt
       rm -f $O/b1bprof/run_kernel_trace.csv ;;
+    pmcb1beam)
+      for f in 1 2; do
+        timeout -s KILL 240 rocprofv3 -i tools/pmc_sq$f.txt --output-format csv -d $O/pq$f -o run -- python3 bench.py --steps 1 --warmup 0 --lanes 1 --batch 4 --latency-repeats 0 --beam5-latency-repeats 1 --latency-warmup 0 --beam5 0 --beam5-steps 0 --realistic-steps 0 --stream-sessions 0 --rest-callers 0 --no-cpu-baseline > $O/pq$f.log 2>&1 || { rc=$?; break; }
+        rc=0
+        python3 tools/pmc_generic.py $O/pq$f/run_counter_collection.csv > $O/pmc_b1beam_$f.txt
+        rm -f $O/pq$f/run_counter_collection.csv
+      done
+      [ $rc -eq 0 ] && grep -A1 "beam_update\|select_kernel" $O/pmc_b1beam_*.txt | head -20 ;;
     repro)
       timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/repro -o run -- ./tools/graph_prof_repro 3 300 2 > $O/repro.log 2>&1
       rc=$?; tail -3 $O/repro.log; rm -f $O/repro/run_kernel_trace.csv ;;

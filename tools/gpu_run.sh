@@ -71,10 +71,12 @@ for s in "$@"; do
       rm -f $O/b1bprof/run_kernel_trace.csv ;;
     pmcb1beam)
       for f in 1 2; do
-        timeout -s KILL 240 rocprofv3 -i tools/pmc_sq$f.txt --output-format csv -d $O/pq$f -o run -- python3 bench.py --steps 1 --warmup 0 --lanes 1 --batch 4 --latency-repeats 0 --beam5-latency-repeats 1 --latency-warmup 0 --beam5 0 --beam5-steps 0 --realistic-steps 0 --stream-sessions 0 --rest-callers 0 --no-cpu-baseline > $O/pq$f.log 2>&1 || { rc=$?; break; }
-        rc=0
-        python3 tools/pmc_generic.py $O/pq$f/run_counter_collection.csv > $O/pmc_b1beam_$f.txt
-        rm -f $O/pq$f/run_counter_collection.csv
+        CN=$(sed -e 's/^pmc: *//' tools/pmc_sq$f.txt)
+        timeout -s KILL 240 rocprofv3 --pmc $CN --output-format csv -d $O/pq$f -o run -- python3 bench.py --steps 1 --warmup 0 --lanes 1 --batch 4 --latency-repeats 0 --beam5-latency-repeats 1 --latency-warmup 0 --beam5 0 --beam5-steps 0 --realistic-steps 0 --stream-sessions 0 --rest-callers 0 --no-cpu-baseline > $O/pq$f.log 2>&1; rc=$?
+        CSV=$(find $O/pq$f -name '*counter_collection.csv' | head -1)
+        [ -n "$CSV" ] && python3 tools/pmc_generic.py $CSV > $O/pmc_b1beam_$f.txt
+        find $O/pq$f -name '*.csv' -delete
+        [ $rc -ne 0 ] && break
       done
       [ $rc -eq 0 ] && grep -A1 "beam_update\|select_kernel" $O/pmc_b1beam_*.txt | head -20 ;;
     repro)

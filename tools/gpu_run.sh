@@ -68,6 +68,7 @@ for s in "$@"; do
     b1beam)
       timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/b1bprof -o run -- python3 bench.py --steps 1 --warmup 0 --lanes 1 --latency-repeats 0 --beam5-latency-repeats 4 --latency-warmup 1 --beam5 0 --beam5-steps 0 --realistic-steps 0 --stream-sessions 0 --rest-callers 0 --no-cpu-baseline > $O/b1beam.json 2> $O/b1beam.err
       rc=$?; [ $rc -eq 0 ] && python3 tools/b1_breakdown.py $O/b1bprof/run_kernel_trace.csv $((5*445)) > $O/b1beam_breakdown.txt && head -40 $O/b1beam_breakdown.txt
+      [ $rc -eq 0 ] && python3 tools/step_timeline.py $O/b1bprof/run_kernel_trace.csv beam_update 1500 > $O/b1beam_step_timeline.txt && cat $O/b1beam_step_timeline.txt
       rm -f $O/b1bprof/run_kernel_trace.csv ;;
     pmcb1beam)
       for f in 1 2; do

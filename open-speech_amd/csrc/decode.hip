@@ -1066,7 +1066,6 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
                                                           int max_tokens) {
     constexpr int MAXC = KM * BEAM_SLICES * 2 * KM;
     constexpr int CPT = (MAXC + 255) / 256;      // candidates per thread
-    constexpr int HPT = (KM * 448 + 255) / 256;  // history / ancestry entries per thread
     __shared__ BeamCand top[2 * KM];
     __shared__ ArgMax wtop[4][2 * KM];
     __shared__ int lseq[KM][448];
@@ -1087,11 +1086,20 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
     // one per phase): both candidate lists of every (row, slice) (the row's timestamp rule,
     // known only once its 16 slice statistics are combined, picks one), the slice
     // statistics, the rows' states, token histories and ancestry.  Clamped addresses.
+    // (flat candidate index i = (k * BEAM_SLICES + slice) * K2 + e: divisions by the runtime
+    // K2 through a float reciprocal, exact with the correction for i < 2^22)
+    const float rk2 = 1.f / (float)K2;
+    auto div_k2 = [&](int x) {
+        int q = (int)((float)x * rk2);
+        q -= q * K2 > x ? 1 : 0;
+        q += (q + 1) * K2 <= x ? 1 : 0;
+        return q;
+    };
     BeamCand ca[CPT], cb[CPT];
 #pragma unroll
     for (int j = 0; j < CPT; ++j) {
-        const int i = min(tid + 256 * j, nc - 1), k = i / (BEAM_SLICES * K2), sl = (i / K2) % BEAM_SLICES;
-        const BeamCand* src = cand + (((int64_t)(r0 + k) * BEAM_SLICES + sl) * 2) * MAXK2 + i % K2;
+        const int i = min(tid + 256 * j, nc - 1), qe = div_k2(i);  // qe = k * BEAM_SLICES + slice
+        const BeamCand* src = cand + ((int64_t)(r0 * BEAM_SLICES + qe) * 2) * MAXK2 + (i - qe * K2);
         ca[j] = src[0];
         cb[j] = src[MAXK2];
     }
@@ -1099,22 +1107,27 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
     if (tid < K * SEL_SPLIT) mp = parts[(int64_t)r0 * SEL_SPLIT + tid];
     SelState ms{};
     if (tid < K) ms = st[r0 + tid];
-    const int nn = max(n, 1), ns = K * nn, na = K * step;
-    int hv[HPT], av[HPT];
+    // token histories and ancestry: row k, positions tid and tid + 256 (both < 448)
+    int hv[KM][2], av[KM][2];
 #pragma unroll
-    for (int j = 0; j < HPT; ++j) {
-        const int i = tid + 256 * j;
-        const int is = min(i, ns - 1), ia = min(i, max(na, 1) - 1);
-        hv[j] = seq[(int64_t)(r0 + is / nn) * max_tokens + min(is % nn, max_tokens - 1)];
-        av[j] = anc[(int64_t)(r0 + ia / max(step, 1)) * ctx + ia % max(step, 1)];
-    }
+    for (int k = 0; k < KM; ++k)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int kk = min(k, K - 1), jj = tid + 256 * h;
+            hv[k][h] = seq[(int64_t)(r0 + kk) * max_tokens + min(jj, min(max(n, 1), max_tokens) - 1)];
+            av[k][h] = anc[(int64_t)(r0 + kk) * ctx + min(jj, max(step, 1) - 1)];
+        }
     if (tid < K * SEL_SPLIT) lparts[tid] = mp;
     if (tid < K) lst[tid] = ms;
 #pragma unroll
-    for (int j = 0; j < HPT; ++j) {
-        const int i = tid + 256 * j;
-        if (i < ns && i % nn < n) lseq[i / nn][i % nn] = hv[j];
-        if (i < na) lanc[i / step][i % step] = av[j];
+    for (int k = 0; k < KM; ++k) {
+        if (k >= K) break;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int jj = tid + 256 * h;
+            if (jj < n) lseq[k][jj] = hv[k][h];
+            if (jj < step) lanc[k][jj] = av[k][h];
+        }
     }
     __syncthreads();
     // per row: lse over the allowed tokens, over the allowed timestamps, and the
@@ -1160,7 +1173,7 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
             cv[j] = -INFINITY;
             cx[j] = INT_MAX;
             if (i < nc) {
-                const int k = i / (BEAM_SLICES * K2);
+                const int k = div_k2(i) / BEAM_SLICES;
                 const BeamCand c = rts[k] ? cb[j] : ca[j];
                 const bool none = c.i == INT_MAX || (first && k != 0);
                 cv[j] = none ? -INFINITY : rsum[k] + (c.s - rlse[k]);

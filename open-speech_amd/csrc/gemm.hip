@@ -1824,15 +1824,12 @@ int launch_gemm_skinny_pro(const GemmArgs& g0, int pro, const ProArgs& pa, bool 
     const int kc = g.K / ks;
     static const bool wb_late = getenv("OSW_PRO_WB_LATE") != nullptr;  // A/B switch
     g.preload_w = wb_late ? 0 : 1;
-    if (pro != PRO_NONE && (pro == PRO_GELU ? g.M > GELU_ROWS || kc > GELU_KC : g.M > PRO_ROWS))
+    if (pro == PRO_GELU ? g.M > GELU_ROWS || kc > GELU_KC : g.M > PRO_ROWS)
         throw std::invalid_argument("fused GEMM prologue: rows or K range exceed its LDS image");
     if (select) {
-        if (!direct || (pro != PRO_RESLN && pro != PRO_NONE) || g.M != 1 || g.epi != EPI_F32 || g.ldc != g.N)
+        if (!direct || pro != PRO_RESLN || g.M != 1 || g.epi != EPI_F32 || g.ldc != g.N)
             throw std::invalid_argument("fused selection: batch-1 logits GEMM only");
-        if (pro == PRO_NONE)  // the row normalised by its own kernel (OSW_B1_LNPOST, A/B)
-            gemm_skinny_kernel<1, true, EPI_F32, true, PRO_NONE, true><<<grid, 256, 0, s>>>(g, kc, part, pa);
-        else
-            gemm_skinny_kernel<1, true, EPI_F32, true, PRO_RESLN, true><<<grid, 256, 0, s>>>(g, kc, part, pa);
+        gemm_skinny_kernel<1, true, EPI_F32, true, PRO_RESLN, true><<<grid, 256, 0, s>>>(g, kc, part, pa);
         return ks;
     }
     if (direct) {

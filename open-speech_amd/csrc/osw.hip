@@ -829,22 +829,6 @@ void decoder_step_fused(osw_ctx* c, int nb, int group, bool gather, const SelFus
     GemmArgs gl = gemm(nullptr, "dec.tok", d.n_vocab, D);
     gl.C = c->logits;
     gl.ldc = d.n_vocab;
-    // OSW_B1_LNPOST=1 (A/B): lnpost by the standalone residual+LayerNorm kernel (one row,
-    // the same resln.h arithmetic) and the selecting logits GEMM without its prologue
-    static const bool ln_kernel = getenv("OSW_B1_LNPOST") != nullptr;
-    if (sf && ln_kernel) {
-        launch_dec_resid_ln(ps[last], ks, nb, D, WF(c, pl + ".fc2.b"), xs[xi], WF(c, "dec.lnpost.g"),
-                            WF(c, "dec.lnpost.b"), c->xdn, lo_d, nullptr, nullptr, nullptr, nullptr, ctx, d.n_vocab,
-                            c->stream, c->row_pos ? 1 : 0);
-        GemmArgs g2 = gemm(c->xdn, "dec.tok", d.n_vocab, D);
-        g2.C = c->logits;
-        g2.ldc = d.n_vocab;
-        ProArgs pa{};
-        pa.sel = *sf;
-        launch_gemm_skinny_pro(g2, PRO_NONE, pa, true, nullptr, c->stream, true);
-        HIPCHK(hipGetLastError());
-        return;
-    }
     ProArgs pl_args = resln(WF(c, pl + ".fc2.b"), "dec.lnpost", false);
     if (sf) pl_args.sel = *sf;
     launch_gemm_skinny_pro(gl, PRO_RESLN, pl_args, true, nullptr, c->stream, sf != nullptr);

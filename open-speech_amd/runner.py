@@ -275,10 +275,10 @@ class _SessionLane(_Worker):
         def answer(t, exc=None):
             req, s, _ = flights.pop(t)
             if not req.fut.done():
-                if exc is None:
+                if exc is None and s is not None:
                     req.fut.set_result(finish_clip(s, req.opts, tok))
                 else:
-                    req.fut.set_exception(exc)
+                    req.fut.set_exception(exc if exc is not None else RuntimeError("request state lost"))
 
         def queue_window(t):
             req, s, _ = flights[t]
@@ -315,10 +315,11 @@ class _SessionLane(_Worker):
                     key, is_open = k, True
                 for r in reqs:
                     tag += 1
-                    flights[tag] = [r, clip_state(0, r.pcm, r.opts, tok), None]
+                    flights[tag] = [r, None, None]
                     try:
+                        flights[tag][1] = clip_state(0, r.pcm, r.opts, tok)
                         queue_window(tag)
-                    except Exception as e:  # noqa: BLE001 - this request's window was refused
+                    except Exception as e:  # noqa: BLE001 - this request (its options or window) was refused
                         if pool.is_device_error(e):
                             raise
                         answer(tag, e)

@@ -252,6 +252,7 @@ def test_concurrent_calls_are_batched():
     holder = []
     b = make_backend(holder=holder)
     b.load_model(MID)
+    holder[0].step_sleep = 0.01   # (continuous default: a session step takes time, so calls overlap)
     res = [None] * 16
 
     def call(i):
@@ -721,5 +722,33 @@ def test_session_lane_switches_keys():
         for r in reqs:
             assert r.fut.result(timeout=30).segments
         assert set(e.cfgs) == {1, 5} and len(e.cfgs) >= 2
+    finally:
+        runner.close()
+
+
+def test_session_lane_bad_option_fails_only_its_request():
+    """An unsupported language fails its own request; the lane's other requests, already
+    decoding in the same session, complete."""
+    from concurrent.futures import Future
+    from open_speech_amd.runner import BatchRunner, _Req
+    from open_speech_amd.segments import TranscribeOptions
+    from open_speech_amd.tokenizer import WhisperTokenizer
+
+    e = FakeEngine(D.MICRO_TEST, 0, 4)
+    e.step_sleep = 0.005
+    runner = BatchRunner([e], WhisperTokenizer(51866), continuous=True)
+    try:
+        good = [_Req(synth.chirp_clip(i, 3.0), TranscribeOptions(language="en"), Future()) for i in range(3)]
+        bad = _Req(synth.chirp_clip(9, 3.0), TranscribeOptions(language="en"), Future())
+        bad.opts.language = "xx"   # same key as the good ones is not required: key() includes language
+        for r in good[:2]:
+            runner.submit_req(r)
+        time.sleep(0.02)
+        runner.submit_req(bad)
+        runner.submit_req(good[2])
+        for r in good:
+            assert r.fut.result(timeout=30).segments
+        with pytest.raises(ValueError, match="unsupported language"):
+            bad.fut.result(timeout=30)
     finally:
         runner.close()

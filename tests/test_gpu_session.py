@@ -154,3 +154,24 @@ def test_session_rejects_other_calls_and_sampling():
         assert len(out) == 1
     finally:
         eng.close()
+
+
+def test_session_end_midway_then_new_session():
+    """A session ended with windows still decoding and queued leaves the context usable: a
+    new session (another decode configuration) and a plain batch decode give the same
+    results as on a fresh context."""
+    d = D.TINY_TEST
+    eng = WhisperEngine(d, device=0, max_batch=4)
+    try:
+        eng.load_weights(weights.random_weights(d, seed=4321, emb_std=0.5))
+        sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+        wins = _windows(d, 9, 500)
+        eng.session_begin(DecodeConfig(suppress_tokens=sup, max_length=64, beam_size=5))
+        eng.session_add(wins)
+        eng.session_step(max_chunks=1)
+        eng.session_end()                     # 4 decoding, 5 queued: dropped
+        cfg = DecodeConfig(suppress_tokens=sup, max_length=64)
+        got = _run_session(eng, cfg, wins[:6])
+        _compare(eng, cfg, wins[:6], got)
+    finally:
+        eng.close()

@@ -218,8 +218,7 @@ typedef struct osw_session_window {
     const int32_t* prefix;    /* <|startofprev|> and the previous tokens, or NULL */
 } osw_session_window;
 int osw_session_begin(osw_ctx* ctx, const osw_decode_opts* opts);
-/* Queue n windows; window i reads clip pcm[offsets[i], offsets[i+1]) (host int16, copied).
- * Windows with seek > 0 (a seek loop's continuations) queue ahead of first windows. */
+/* Queue n windows; window i reads clip pcm[offsets[i], offsets[i+1]) (host int16, copied). */
 int osw_session_add(osw_ctx* ctx, const int16_t* pcm, const int64_t* offsets, int32_t n,
                     const osw_session_window* windows);
 /* Admit queued windows into free slots (when at least min(refill_min, queued) slots are

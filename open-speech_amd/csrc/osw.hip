@@ -1570,16 +1570,7 @@ void session_add(osw_ctx* c, const int16_t* pcm, const int64_t* offsets, int n, 
         q.prefix.assign(w[i].prefix, w[i].prefix + w[i].n_prefix);
         q.w = w[i];
         q.w.prefix = nullptr;
-        // a window past a clip's start continues a seek loop already under way: it queues
-        // behind the other continuations but ahead of first windows, so a long file's tail
-        // is not held behind every request that arrived after it
-        if (q.w.seek > 0) {
-            auto it = S->queue.begin();
-            while (it != S->queue.end() && it->w.seek > 0) ++it;
-            S->queue.insert(it, std::move(q));
-        } else {
-            S->queue.push_back(std::move(q));
-        }
+        S->queue.push_back(std::move(q));
     }
 }
 

@@ -1057,6 +1057,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void s
 // pick the surviving beams and reorder their tokens / ancestry / state.
 // KM: the largest beam the LDS arrays hold (5, the reference's beam_size: 24 KiB, so the
 // workgroup fits beside another lane's 128-KiB encoder workgroup; 8: 45 KiB)
+#ifdef OSW_STAMPS
+// diagnostic build only (make EXTRA=-DOSW_STAMPS): phase times of the last beam_update launch's
+// workgroup 0, read by osw_debug_stamps (never part of the product library)
+__device__ unsigned long long osw_stamps[16];
+#define OSW_STAMP(i)                                                                        \
+    do {                                                                                    \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+        unsigned long long t_;                                                              \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+        if (blockIdx.x == 0 && threadIdx.x == 0) osw_stamps[i] = t_;                        \
+    } while (0)
+#else
+#define OSW_STAMP(i) \
+    do {             \
+    } while (0)
+#endif
+
 template <int KM>
 __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* __restrict__ pos_ptr,
                                                           SelState* __restrict__ st, const SelPart* __restrict__ parts,
@@ -1073,11 +1091,13 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
     __shared__ SelState lst[KM];
     __shared__ SelPart lparts[KM * SEL_SPLIT];
     __shared__ int choose[KM], fin, best_src, best_extra, improved;
+    OSW_STAMP(0);
     const int w = blockIdx.x, tid = threadIdx.x, K = P.beam, K2 = 2 * K;
     const int r0 = w * K;
     const int step = pos_ptr[P.pos_row ? r0 : 0];
     const SelState s0 = st[r0];
     if (sel_mode(P, step, s0) != SEL_SAMPLE) return;
+    OSW_STAMP(1);
     const int nc = K * BEAM_SLICES * K2;
     const int n = s0.n_sampled;  // identical for every row of the window
     const int plen = row_plen(P, s0);
@@ -1130,6 +1150,7 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
         }
     }
     __syncthreads();
+    OSW_STAMP(2);
     // per row: lse over the allowed tokens, over the allowed timestamps, and the
     // timestamp-mass rule (the row's 16 slice statistics merged in fixed order, as
     // combine_parts does)
@@ -1154,6 +1175,7 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
         rts[tid] = ts_wins;
     }
     __syncthreads();
+    OSW_STAMP(3);
     {
         // the top K2 candidates by (score desc, flat id asc), NaN scores and INT_MAX ids
         // excluded, {-inf, INT_MAX} past the last valid one.  Each wave pops its own top K2
@@ -1223,6 +1245,7 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
         }
         __syncthreads();
     }
+    OSW_STAMP(4);
     if (tid == 0) {
         BeamWin bw = bwin[w];
         // the last step: max_length, or (length control) the window's token budget
@@ -1264,6 +1287,7 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
         bwin[w] = bw;
     }
     __syncthreads();
+    OSW_STAMP(5);
     if (improved) {
         int* dst = best_tok + (int64_t)w * max_tokens;
         for (int j = tid; j < n && j < max_tokens; j += 256) dst[j] = lseq[best_src][j];
@@ -1298,6 +1322,7 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
             cur_tok[r0 + k] = tok;
         }
     }
+    OSW_STAMP(6);
 }
 
 // grid windows: the per-window merge / finish / reorder, then an arrival count over
@@ -1313,6 +1338,7 @@ __global__ __launch_bounds__(256) void beam_update_kernel(SelParams P, int* __re
     const int step = pos_ptr[P.pos_row ? blockIdx.x * P.beam : 0];
     beam_update_body<KM>(P, pos_ptr, st, parts, cand, seq, anc, ctx, bwin, best_tok, cur_tok, max_tokens);
     __syncthreads();
+    OSW_STAMP(7);
     if (P.pos_row) {  // a session: this window's rows advance their own counters
         if (threadIdx.x < P.beam) pos_ptr[blockIdx.x * P.beam + threadIdx.x] = step + 1;
         return;
@@ -1509,3 +1535,10 @@ void launch_count_done(const SelState* st, int rows, int* out, hipStream_t s) {
 
 
 }  // namespace osw
+
+#ifdef OSW_STAMPS
+extern "C" int osw_debug_stamps(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(osw::osw_stamps), sizeof(unsigned long long) * 16, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif

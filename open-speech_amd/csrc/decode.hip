@@ -1058,8 +1058,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void s
 // KM: the largest beam the LDS arrays hold (5, the reference's beam_size: 24 KiB, so the
 // workgroup fits beside another lane's 128-KiB encoder workgroup; 8: 45 KiB)
 #ifdef OSW_STAMPS
-// diagnostic build only (make EXTRA=-DOSW_STAMPS): phase times of the last beam_update launch's
-// workgroup 0, read by osw_debug_stamps (never part of the product library)
+// diagnostic build only (make EXTRA=-DOSW_STAMPS): phase times of the last beam_update launch
+// whose workgroup 0 ran the whole update (staged in [8, 15)), read by osw_debug_stamps (never
+// part of the product library)
 __device__ unsigned long long osw_stamps[16];
 #define OSW_STAMP(i)                                                                        \
     do {                                                                                    \
@@ -1067,7 +1068,15 @@ __device__ unsigned long long osw_stamps[16];
         unsigned long long t_;                                                              \
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
         __builtin_amdgcn_sched_barrier(0);                                                  \
-        if (blockIdx.x == 0 && threadIdx.x == 0) osw_stamps[i] = t_;                        \
+        if (blockIdx.x == 0 && threadIdx.x == 0) {                                          \
+            if ((i) < 7) osw_stamps[8 + (i)] = t_;                                          \
+            if ((i) == 6) osw_stamps[15] = 1; /* this launch took the full path */          \
+            if ((i) == 7 && osw_stamps[15]) {                                               \
+                for (int j_ = 0; j_ < 7; ++j_) osw_stamps[j_] = osw_stamps[8 + j_];         \
+                osw_stamps[7] = t_;                                                         \
+                osw_stamps[15] = 0;                                                         \
+            }                                                                               \
+        }                                                                                   \
     } while (0)
 #else
 #define OSW_STAMP(i) \

@@ -1059,28 +1059,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void s
 // workgroup fits beside another lane's 128-KiB encoder workgroup; 8: 45 KiB)
 #ifdef OSW_STAMPS
 // diagnostic build only (make EXTRA=-DOSW_STAMPS): phase times of the last beam_update launch
-// whose workgroup 0 ran the whole update (staged in [8, 15)), read by osw_debug_stamps (never
-// part of the product library)
-__device__ unsigned long long osw_stamps[16];
+// whose workgroup 0 ran the whole update (staged in [16, 28), flag 31), read by
+// osw_debug_stamps (never part of the product library).  OSW_STAMP_LAST closes a launch.
+__device__ unsigned long long osw_stamps[32];
 #define OSW_STAMP(i)                                                                        \
     do {                                                                                    \
         __builtin_amdgcn_sched_barrier(0);                                                  \
         unsigned long long t_;                                                              \
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
         __builtin_amdgcn_sched_barrier(0);                                                  \
-        if (blockIdx.x == 0 && threadIdx.x == 0) {                                          \
-            if ((i) < 7) osw_stamps[8 + (i)] = t_;                                          \
-            if ((i) == 6) osw_stamps[15] = 1; /* this launch took the full path */          \
-            if ((i) == 7 && osw_stamps[15]) {                                               \
-                for (int j_ = 0; j_ < 7; ++j_) osw_stamps[j_] = osw_stamps[8 + j_];         \
-                osw_stamps[7] = t_;                                                         \
-                osw_stamps[15] = 0;                                                         \
-            }                                                                               \
+        if (blockIdx.x == 0 && threadIdx.x == 0) osw_stamps[16 + (i)] = t_;                 \
+    } while (0)
+#define OSW_STAMP_FULL()                                                                    \
+    do {                                                                                    \
+        if (blockIdx.x == 0 && threadIdx.x == 0) osw_stamps[31] = 1;                        \
+    } while (0)
+#define OSW_STAMP_LAST(i)                                                                   \
+    do {                                                                                    \
+        OSW_STAMP(i);                                                                       \
+        if (blockIdx.x == 0 && threadIdx.x == 0 && osw_stamps[31]) {                        \
+            for (int j_ = 0; j_ <= (i); ++j_) osw_stamps[j_] = osw_stamps[16 + j_];         \
+            osw_stamps[31] = 0;                                                             \
         }                                                                                   \
     } while (0)
 #else
 #define OSW_STAMP(i) \
     do {             \
+    } while (0)
+#define OSW_STAMP_FULL() \
+    do {                 \
+    } while (0)
+#define OSW_STAMP_LAST(i) \
+    do {                  \
     } while (0)
 #endif
 
@@ -1094,11 +1104,10 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
     constexpr int MAXC = KM * BEAM_SLICES * 2 * KM;
     constexpr int CPT = (MAXC + 255) / 256;      // candidates per thread
     __shared__ BeamCand top[2 * KM];
-    __shared__ ArgMax wtop[4][2 * KM];
+    __shared__ ArgMax wtop[4 * 2 * KM];
     __shared__ int lseq[KM][448];
     __shared__ int lanc[KM][448];
     __shared__ SelState lst[KM];
-    __shared__ SelPart lparts[KM * SEL_SPLIT];
     __shared__ int choose[KM], fin, best_src, best_extra, improved;
     OSW_STAMP(0);
     const int w = blockIdx.x, tid = threadIdx.x, K = P.beam, K2 = 2 * K;
@@ -1146,7 +1155,6 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
             hv[k][h] = seq[(int64_t)(r0 + kk) * max_tokens + min(jj, min(max(n, 1), max_tokens) - 1)];
             av[k][h] = anc[(int64_t)(r0 + kk) * ctx + min(jj, max(step, 1) - 1)];
         }
-    if (tid < K * SEL_SPLIT) lparts[tid] = mp;
     if (tid < K) lst[tid] = ms;
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
@@ -1158,95 +1166,142 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
             if (jj < step) lanc[k][jj] = av[k][h];
         }
     }
-    __syncthreads();
-    OSW_STAMP(2);
     // per row: lse over the allowed tokens, over the allowed timestamps, and the
-    // timestamp-mass rule (the row's 16 slice statistics merged in fixed order, as
-    // combine_parts does)
+    // timestamp-mass rule.  Lane k * SEL_SPLIT + slice holds slice statistics of row k; a
+    // butterfly merges the row's 16 (lse_merge and amax commute, so every lane of the group
+    // ends with the same statistics)
+    static_assert(SEL_SPLIT == 16, "one 16-lane DPP row per beam row");
     __shared__ float rlse[KM], rsum[KM];
     __shared__ int rts[KM];
-    if (tid < K) {
-        rsum[tid] = lst[tid].sum_lp;
-        SelPart r = lparts[tid * SEL_SPLIT];
-        for (int i = 1; i < SEL_SPLIT; ++i) {
-            const SelPart q = lparts[tid * SEL_SPLIT + i];
-            lse_merge(r.m_all, r.s_all, q.m_all, q.s_all);
-            lse_merge(r.m_ts, r.s_ts, q.m_ts, q.s_ts);
-            ArgMax A = amax(ArgMax{r.v_all, r.i_all}, ArgMax{q.v_all, q.i_all});
-            ArgMax X = amax(ArgMax{r.v_text, r.i_text}, ArgMax{q.v_text, q.i_text});
-            ArgMax T = amax(ArgMax{r.v_ts, r.i_ts}, ArgMax{q.v_ts, q.i_ts});
-            r.v_all = A.v; r.i_all = A.i; r.v_text = X.v; r.i_text = X.i; r.v_ts = T.v; r.i_ts = T.i;
+    {
+        float m_all = mp.m_all, s_all = mp.s_all, m_ts = mp.m_ts, s_ts = mp.s_ts;
+        ArgMax X{mp.v_text, mp.i_text};
+        auto bfly = [&](auto o) {
+            constexpr int O = decltype(o)::value;
+            const float ma = xor_lane<O>(m_all), sa = xor_lane<O>(s_all);
+            const float mt = xor_lane<O>(m_ts), stt = xor_lane<O>(s_ts);
+            const ArgMax x{xor_lane<O>(X.v), xor_lane<O>(X.i)};
+            lse_merge(m_all, s_all, ma, sa);
+            lse_merge(m_ts, s_ts, mt, stt);
+            X = amax(X, x);
+        };
+        bfly(IC<1>{}), bfly(IC<2>{}), bfly(IC<4>{}), bfly(IC<8>{});
+        if (tid < K * SEL_SPLIT && (tid & (SEL_SPLIT - 1)) == 0) {
+            const int k = tid / SEL_SPLIT;
+            const float lse_all = m_all + logf(s_all);
+            const float lse_ts = m_ts == -INFINITY ? -INFINITY : m_ts + logf(s_ts);
+            const bool ts_wins = P.with_ts && lse_ts - lse_all > X.v - lse_all;
+            rlse[k] = ts_wins ? lse_ts : lse_all;
+            rts[k] = ts_wins;
         }
-        const float lse_all = r.m_all + logf(r.s_all);
-        const float lse_ts = r.m_ts == -INFINITY ? -INFINITY : r.m_ts + logf(r.s_ts);
-        const bool ts_wins = P.with_ts && lse_ts - lse_all > r.v_text - lse_all;
-        rlse[tid] = ts_wins ? lse_ts : lse_all;
-        rts[tid] = ts_wins;
+        if (tid < K) rsum[tid] = ms.sum_lp;
     }
     __syncthreads();
+    OSW_STAMP(2);
     OSW_STAMP(3);
     {
         // the top K2 candidates by (score desc, flat id asc), NaN scores and INT_MAX ids
         // excluded, {-inf, INT_MAX} past the last valid one.  Each wave pops its own top K2
-        // from registers (wave argmax, no barrier; flat ids are unique, so one lane owns
-        // each pop), then wave 0 ranks the 4*K2 survivors: the global top K2 lie among
-        // them, so this is the list (and order) of K2 block-wide pops, with one barrier
-        // instead of 2*K2.
+        // (wave max of the lanes' best scores, a ballot for ties; flat ids are unique, so
+        // one lane owns each pop and shifts its sorted list), then wave 0 ranks the 4*K2
+        // survivors: the global top K2 lie among them, so this is the list (and order) of
+        // K2 block-wide pops, with one barrier instead of 2*K2.
         const int lane = tid & 63, wv = tid >> 6;
         // candidate (row k, slice, j): list B if the row's timestamps win, else list A; score =
         // sum_lp + (x - lse) as the per-row log-prob + cumulative score of the reference
+        // ck: the score as an int ordered like the float (-0 as +0; dead: INT_MIN), so wave
+        // maxima are integer DPP maxima and equal keys are equal scores
         float cv[CPT];
-        int cx[CPT];
-        unsigned live = 0;
+        int cx[CPT], ck[CPT];
 #pragma unroll
         for (int j = 0; j < CPT; ++j) {
             const int i = tid + 256 * j;
             cv[j] = -INFINITY;
             cx[j] = INT_MAX;
+            ck[j] = INT_MIN;
             if (i < nc) {
                 const int k = div_k2(i) / BEAM_SLICES;
                 const BeamCand c = rts[k] ? cb[j] : ca[j];
-                const bool none = c.i == INT_MAX || (first && k != 0);
-                cv[j] = none ? -INFINITY : rsum[k] + (c.s - rlse[k]);
-                cx[j] = none ? INT_MAX : k * P.V + c.i;
-                if (cx[j] != INT_MAX && !(cv[j] != cv[j])) live |= 1u << j;
-            }
-        }
-        int at = -1;
-        auto mine = [&]() {
-            ArgMax a{-INFINITY, INT_MAX};
-            at = -1;
-#pragma unroll
-            for (int j = 0; j < CPT; ++j)
-                if ((live >> j) & 1u) {
-                    const ArgMax m = amax(a, ArgMax{cv[j], cx[j]});
-                    if (m.i != a.i || m.v != a.v) { a = m; at = j; }
+                const float v = rsum[k] + (c.s - rlse[k]);
+                if (c.i != INT_MAX && !(first && k != 0) && !(v != v)) {
+                    cv[j] = v;
+                    cx[j] = k * P.V + c.i;
+                    const int u = __float_as_int(v == 0.f ? 0.f : v);
+                    ck[j] = u ^ ((u >> 31) & 0x7fffffff);
                 }
-            return a;
-        };
-        ArgMax my = mine();
-        for (int r = 0; r < K2; ++r) {
-            ArgMax a = my;
-            auto stp = [&](auto o) {
-                constexpr int O = decltype(o)::value;
-                a = amax(a, ArgMax{xor_lane<O>(a.v), xor_lane<O>(a.i)});
-            };
-            stp(IC<32>{}), stp(IC<16>{}), stp(IC<8>{}), stp(IC<4>{}), stp(IC<2>{}), stp(IC<1>{});
-            if (lane == 0) wtop[wv][r] = a;
-            if (a.i != INT_MAX && at >= 0 && my.i == a.i) {
-                live &= ~(1u << at);
-                my = mine();
             }
         }
+        // this lane's candidates best first (amax order)
+#pragma unroll
+        for (int a = 1; a < CPT; ++a)
+#pragma unroll
+            for (int b = a; b > 0; --b) {
+                const bool sw = ck[b] > ck[b - 1] || (ck[b] == ck[b - 1] && cx[b] < cx[b - 1]);
+                const float tv = cv[b];
+                const int ti = cx[b], tk = ck[b];
+                cv[b] = sw ? cv[b - 1] : tv;
+                cx[b] = sw ? cx[b - 1] : ti;
+                ck[b] = sw ? ck[b - 1] : tk;
+                cv[b - 1] = sw ? tv : cv[b - 1];
+                cx[b - 1] = sw ? ti : cx[b - 1];
+                ck[b - 1] = sw ? tk : ck[b - 1];
+            }
+        for (int r = 0; r < K2; ++r) {
+            int m = ck[0];
+            m = max(m, xor_lane<32>(m));
+            m = max(m, xor_lane<16>(m));
+            m = max(m, xor_lane<8>(m));
+            m = max(m, xor_lane<4>(m));
+            m = max(m, xor_lane<2>(m));
+            m = max(m, xor_lane<1>(m));
+            const unsigned long long tie = __ballot(ck[0] == m);
+            int owner = __ffsll((long long)tie) - 1;
+            if (__popcll(tie) > 1) {  // equal scores: the smallest flat id
+                int im = ck[0] == m ? cx[0] : INT_MAX;
+                im = min(im, xor_lane<32>(im));
+                im = min(im, xor_lane<16>(im));
+                im = min(im, xor_lane<8>(im));
+                im = min(im, xor_lane<4>(im));
+                im = min(im, xor_lane<2>(im));
+                im = min(im, xor_lane<1>(im));
+                owner = __ffsll((long long)__ballot(ck[0] == m && cx[0] == im)) - 1;
+            }
+            if (lane == 0)
+                wtop[wv * K2 + r] = ArgMax{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(cv[0]), owner)),
+                                           __builtin_amdgcn_readlane(cx[0], owner)};
+            if (lane == owner) {
+#pragma unroll
+                for (int j = 0; j + 1 < CPT; ++j) {
+                    cv[j] = cv[j + 1];
+                    cx[j] = cx[j + 1];
+                    ck[j] = ck[j + 1];
+                }
+                cv[CPT - 1] = -INFINITY;
+                cx[CPT - 1] = INT_MAX;
+                ck[CPT - 1] = INT_MIN;
+            }
+        }
+        OSW_STAMP(4);
         __syncthreads();
+        OSW_STAMP(5);
         if (wv == 0) {
             const int S = 4 * K2;  // <= 64 (K2 <= 2 * KM <= 16)
-            const ArgMax e = lane < S ? wtop[lane / K2][lane % K2] : ArgMax{-INFINITY, INT_MAX};
+            const ArgMax e = lane < S ? wtop[lane] : ArgMax{-INFINITY, INT_MAX};
             const bool valid = lane < S && e.i != INT_MAX;
+            // rank = #survivors before e in amax order, by one unsigned 64-bit key per
+            // survivor (ordered score, then ~id; 0 for none)
+            const int u = __float_as_int(e.v == 0.f ? 0.f : e.v);
+            const unsigned long long key =
+                valid ? ((unsigned long long)((unsigned)(u ^ ((u >> 31) & 0x7fffffff)) ^ 0x80000000u) << 32) |
+                            (unsigned)~e.i
+                      : 0ull;
+            const unsigned klo = (unsigned)key, khi = (unsigned)(key >> 32);
             int rank = 0;
+#pragma unroll 4
             for (int j = 0; j < S; ++j) {
-                const ArgMax f = wtop[j / K2][j % K2];
-                rank += (f.i != INT_MAX && (f.v > e.v || (f.v == e.v && f.i < e.i))) ? 1 : 0;
+                const unsigned long long f = ((unsigned long long)__builtin_amdgcn_readlane(khi, j) << 32) |
+                                             (unsigned)__builtin_amdgcn_readlane(klo, j);
+                rank += f > key ? 1 : 0;
             }
             const int nvalid = __popcll(__ballot(valid));
             if (valid && rank < K2) top[rank] = BeamCand{e.v, e.i};
@@ -1254,7 +1309,7 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
         }
         __syncthreads();
     }
-    OSW_STAMP(4);
+    OSW_STAMP(6);
     if (tid == 0) {
         BeamWin bw = bwin[w];
         // the last step: max_length, or (length control) the window's token budget
@@ -1296,7 +1351,7 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
         bwin[w] = bw;
     }
     __syncthreads();
-    OSW_STAMP(5);
+    OSW_STAMP(7);
     if (improved) {
         int* dst = best_tok + (int64_t)w * max_tokens;
         for (int j = tid; j < n && j < max_tokens; j += 256) dst[j] = lseq[best_src][j];
@@ -1311,27 +1366,42 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
         }
         return;
     }
-    for (int k = 0; k < K; ++k) {
-        const BeamCand c = top[choose[k]];
-        const int q = c.i == INT_MAX ? 0 : c.i / P.V;
-        const int tok = c.i == INT_MAX ? P.eot : c.i % P.V;
+    // row k continues hypothesis top[choose[k]]: its source row's history (positions tid and
+    // tid + 256, both < 448) and ancestry, then the state (thread k)
+    int qk[KM];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+        const int c = top[choose[min(k, K - 1)]].i;
+        qk[k] = c == INT_MAX ? 0 : c / P.V;
+    }
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+        if (k >= K) break;
         int* sq = seq + (int64_t)(r0 + k) * max_tokens;
-        for (int j = tid; j < n && j < max_tokens; j += 256) sq[j] = lseq[q][j];
         int* an = anc + (int64_t)(r0 + k) * ctx;
-        for (int p = tid; p <= step && p < ctx; p += 256) an[p] = p < step ? lanc[q][p] : r0 + q;
-        if (tid == 0) {
-            if (n < max_tokens) sq[n] = tok;
-            SelState s2 = lst[q];
-            s2.n_sampled = n + 1;
-            s2.penult = s2.last;
-            s2.last = tok;
-            if (tok >= P.tb) s2.last_ts = tok;
-            s2.sum_lp = c.s;
-            st[r0 + k] = s2;
-            cur_tok[r0 + k] = tok;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int j = tid + 256 * h;
+            if (j < n && j < max_tokens) sq[j] = lseq[qk[k]][j];
+            if (j <= step && j < ctx) an[j] = j < step ? lanc[qk[k]][j] : r0 + qk[k];
         }
     }
-    OSW_STAMP(6);
+    if (tid < K) {
+        const BeamCand c = top[choose[tid]];
+        const int q = c.i == INT_MAX ? 0 : c.i / P.V;
+        const int tok = c.i == INT_MAX ? P.eot : c.i % P.V;
+        if (n < max_tokens) seq[(int64_t)(r0 + tid) * max_tokens + n] = tok;
+        SelState s2 = lst[q];
+        s2.n_sampled = n + 1;
+        s2.penult = s2.last;
+        s2.last = tok;
+        if (tok >= P.tb) s2.last_ts = tok;
+        s2.sum_lp = c.s;
+        st[r0 + tid] = s2;
+        cur_tok[r0 + tid] = tok;
+    }
+    OSW_STAMP(8);
+    OSW_STAMP_FULL();
 }
 
 // grid windows: the per-window merge / finish / reorder, then an arrival count over
@@ -1347,7 +1417,7 @@ __global__ __launch_bounds__(256) void beam_update_kernel(SelParams P, int* __re
     const int step = pos_ptr[P.pos_row ? blockIdx.x * P.beam : 0];
     beam_update_body<KM>(P, pos_ptr, st, parts, cand, seq, anc, ctx, bwin, best_tok, cur_tok, max_tokens);
     __syncthreads();
-    OSW_STAMP(7);
+    OSW_STAMP_LAST(9);
     if (P.pos_row) {  // a session: this window's rows advance their own counters
         if (threadIdx.x < P.beam) pos_ptr[blockIdx.x * P.beam + threadIdx.x] = step + 1;
         return;
@@ -1547,7 +1617,7 @@ void launch_count_done(const SelState* st, int rows, int* out, hipStream_t s) {
 
 #ifdef OSW_STAMPS
 extern "C" int osw_debug_stamps(unsigned long long* out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(osw::osw_stamps), sizeof(unsigned long long) * 16, 0,
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(osw::osw_stamps), sizeof(unsigned long long) * 32, 0,
                                hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -21,17 +21,19 @@ from open_speech_amd.tokenizer import WhisperTokenizer, get_suppressed_tokens  #
 eng = WhisperEngine(D.LARGE_V3_TURBO, device=0, max_batch=1)
 eng.init_random(seed=0)
 sup = get_suppressed_tokens(WhisperTokenizer(51866), [-1])
-names = ["entry", "state loaded", "loads in LDS", "rows combined", "top 2K", "finish bookkeeping",
-         "write-back", "kernel tail"]
+names = ["entry", "state loaded", "loads in LDS", "rows combined", "wave pops", "pops barrier",
+         "ranking", "finish bookkeeping", "write-back", "kernel tail"]
+N = len(names)
 lib = _lib.load()
 fn = lib.osw_debug_stamps
 fn.argtypes = [C.POINTER(C.c_ulonglong)]
 for budget in (40, 200, 400):
     cfg = DecodeConfig(suppress_tokens=sup, beam_size=5, max_length=448, token_budget=(budget,))
     eng.transcribe_batch([synth.chirp_clip(1, 30.0)], cfg)
-    buf = (C.c_ulonglong * 16)()
+    buf = (C.c_ulonglong * 32)()
     assert fn(buf) == 0
-    t = np.array(buf[:8], dtype=np.int64)
+    t = np.array(buf[:N], dtype=np.int64)
     d = np.diff(t)
-    print(f"budget {budget}: total {t[7] - t[0]} cycles; " + ", ".join(f"{names[i + 1]} +{d[i]}" for i in range(7)))
+    print(f"budget {budget}: total {t[N - 1] - t[0]} cycles; "
+          + ", ".join(f"{names[i + 1]} +{d[i]}" for i in range(N - 1)))
 eng.close()

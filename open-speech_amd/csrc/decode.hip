@@ -1108,22 +1108,19 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
     __shared__ int lseq[KM][448];
     __shared__ int lanc[KM][448];
     __shared__ SelState lst[KM];
-    __shared__ int choose[KM], fin, best_src, best_extra, improved;
+    __shared__ int ch_src[KM], ch_tok[KM], fin, best_src, best_extra, improved;
+    __shared__ float ch_score[KM];
     OSW_STAMP(0);
     const int w = blockIdx.x, tid = threadIdx.x, K = P.beam, K2 = 2 * K;
     const int r0 = w * K;
     const int step = pos_ptr[P.pos_row ? r0 : 0];
     const SelState s0 = st[r0];
-    if (sel_mode(P, step, s0) != SEL_SAMPLE) return;
-    OSW_STAMP(1);
     const int nc = K * BEAM_SLICES * K2;
-    const int n = s0.n_sampled;  // identical for every row of the window
-    const int plen = row_plen(P, s0);
-    const bool first = step == plen - 1;  // only the prompt hypothesis expands
-    // Every load of the update is issued before any is used (one memory round trip instead of
-    // one per phase): both candidate lists of every (row, slice) (the row's timestamp rule,
-    // known only once its 16 slice statistics are combined, picks one), the slice
-    // statistics, the rows' states, token histories and ancestry.  Clamped addresses.
+    // Loads are issued before any is used, in two round trips: with the window's state (before
+    // its mode is known; wasted only by a window that is not sampling) both candidate lists of
+    // every (row, slice) (the row's timestamp rule, known only once its 16 slice statistics
+    // are combined, picks one), the slice statistics and the rows' states; then the token
+    // histories and ancestry, whose extents need the state.  Clamped addresses.
     // (flat candidate index i = (k * BEAM_SLICES + slice) * K2 + e: divisions by the runtime
     // K2 through a float reciprocal, exact with the correction for i < 2^22)
     const float rk2 = 1.f / (float)K2;
@@ -1145,6 +1142,17 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
     if (tid < K * SEL_SPLIT) mp = parts[(int64_t)r0 * SEL_SPLIT + tid];
     SelState ms{};
     if (tid < K) ms = st[r0 + tid];
+    BeamWin bw{};  // the window's finished-hypothesis record and token budget (thread 0)
+    int budget = 0;
+    if (tid == 0) {
+        bw = bwin[w];
+        budget = P.budget ? P.budget[r0] : 0;
+    }
+    if (sel_mode(P, step, s0) != SEL_SAMPLE) return;
+    OSW_STAMP(1);
+    const int n = s0.n_sampled;  // identical for every row of the window
+    const int plen = row_plen(P, s0);
+    const bool first = step == plen - 1;  // only the prompt hypothesis expands
     // token histories and ancestry: row k, positions tid and tid + 256 (both < 448)
     int hv[KM][2], av[KM][2];
 #pragma unroll
@@ -1211,12 +1219,11 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
         // sum_lp + (x - lse) as the per-row log-prob + cumulative score of the reference
         // ck: the score as an int ordered like the float (-0 as +0; dead: INT_MIN), so wave
         // maxima are integer DPP maxima and equal keys are equal scores
-        float cv[CPT];
+        // (an involution: the score is read back from the key)
         int cx[CPT], ck[CPT];
 #pragma unroll
         for (int j = 0; j < CPT; ++j) {
             const int i = tid + 256 * j;
-            cv[j] = -INFINITY;
             cx[j] = INT_MAX;
             ck[j] = INT_MIN;
             if (i < nc) {
@@ -1224,7 +1231,6 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
                 const BeamCand c = rts[k] ? cb[j] : ca[j];
                 const float v = rsum[k] + (c.s - rlse[k]);
                 if (c.i != INT_MAX && !(first && k != 0) && !(v != v)) {
-                    cv[j] = v;
                     cx[j] = k * P.V + c.i;
                     const int u = __float_as_int(v == 0.f ? 0.f : v);
                     ck[j] = u ^ ((u >> 31) & 0x7fffffff);
@@ -1237,23 +1243,23 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
 #pragma unroll
             for (int b = a; b > 0; --b) {
                 const bool sw = ck[b] > ck[b - 1] || (ck[b] == ck[b - 1] && cx[b] < cx[b - 1]);
-                const float tv = cv[b];
                 const int ti = cx[b], tk = ck[b];
-                cv[b] = sw ? cv[b - 1] : tv;
                 cx[b] = sw ? cx[b - 1] : ti;
                 ck[b] = sw ? ck[b - 1] : tk;
-                cv[b - 1] = sw ? tv : cv[b - 1];
                 cx[b - 1] = sw ? ti : cx[b - 1];
                 ck[b - 1] = sw ? tk : ck[b - 1];
             }
         for (int r = 0; r < K2; ++r) {
-            int m = ck[0];
-            m = max(m, xor_lane<32>(m));
-            m = max(m, xor_lane<16>(m));
-            m = max(m, xor_lane<8>(m));
-            m = max(m, xor_lane<4>(m));
-            m = max(m, xor_lane<2>(m));
-            m = max(m, xor_lane<1>(m));
+            // wave maximum into lane 63: row shifts 1, 2, 4, 8 (lane 15 of each row holds the
+            // row's maximum), then row broadcasts 15 and 31 (lanes without a source see INT_MIN)
+            int t = ck[0];
+            t = max(t, __builtin_amdgcn_update_dpp(INT_MIN, t, 0x111, 0xf, 0xf, false));  // row_shr:1
+            t = max(t, __builtin_amdgcn_update_dpp(INT_MIN, t, 0x112, 0xf, 0xf, false));  // row_shr:2
+            t = max(t, __builtin_amdgcn_update_dpp(INT_MIN, t, 0x114, 0xf, 0xf, false));  // row_shr:4
+            t = max(t, __builtin_amdgcn_update_dpp(INT_MIN, t, 0x118, 0xf, 0xf, false));  // row_shr:8
+            t = max(t, __builtin_amdgcn_update_dpp(INT_MIN, t, 0x142, 0xa, 0xf, false));  // row_bcast:15
+            t = max(t, __builtin_amdgcn_update_dpp(INT_MIN, t, 0x143, 0xc, 0xf, false));  // row_bcast:31
+            const int m = __builtin_amdgcn_readlane(t, 63);
             const unsigned long long tie = __ballot(ck[0] == m);
             int owner = __ffsll((long long)tie) - 1;
             if (__popcll(tie) > 1) {  // equal scores: the smallest flat id
@@ -1267,16 +1273,14 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
                 owner = __ffsll((long long)__ballot(ck[0] == m && cx[0] == im)) - 1;
             }
             if (lane == 0)
-                wtop[wv * K2 + r] = ArgMax{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(cv[0]), owner)),
+                wtop[wv * K2 + r] = ArgMax{__int_as_float(m ^ ((m >> 31) & 0x7fffffff)),
                                            __builtin_amdgcn_readlane(cx[0], owner)};
             if (lane == owner) {
 #pragma unroll
                 for (int j = 0; j + 1 < CPT; ++j) {
-                    cv[j] = cv[j + 1];
                     cx[j] = cx[j + 1];
                     ck[j] = ck[j + 1];
                 }
-                cv[CPT - 1] = -INFINITY;
                 cx[CPT - 1] = INT_MAX;
                 ck[CPT - 1] = INT_MIN;
             }
@@ -1310,45 +1314,61 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
         __syncthreads();
     }
     OSW_STAMP(6);
-    if (tid == 0) {
-        BeamWin bw = bwin[w];
-        // the last step: max_length, or (length control) the window's token budget
-        const bool is_last = plen + n + 1 >= P.max_length || (P.budget && P.budget[r0] > 0 && n + 1 >= P.budget[r0]);
-        int sec = K;
-        bool top_fin = false;
-        improved = 0;
-        for (int k = 0; k < K; ++k) {
-            const BeamCand c = top[k];
-            const int tok = c.i == INT_MAX ? P.eot : c.i % P.V;
-            int nb = k;
-            if (tok == P.eot || is_last) {
-                if (k == 0) top_fin = true;
-                const int len = n + (tok == P.eot ? 0 : 1);
-                const float norm = len == 0 ? (P.length_penalty != 0.f ? -INFINITY : c.s)
-                                            : c.s / powf((float)len, P.length_penalty);
-                bw.n_hyp += 1;
-                if (bw.n_hyp == 1 || norm > bw.best_norm) {
-                    bw.best_norm = norm;
-                    bw.best_raw = c.s;
-                    bw.best_len = min(len, max_tokens);
-                    best_src = c.i == INT_MAX ? 0 : c.i / P.V;
-                    best_extra = tok == P.eot ? -1 : tok;
-                    improved = 1;
-                }
-                for (int j = sec; j < K2; ++j) {
-                    const int t2 = top[j].i == INT_MAX ? P.eot : top[j].i % P.V;
-                    if (t2 != P.eot) {
-                        nb = j;
-                        sec = j + 1;
-                        break;
+    if (tid < 64) {
+        // wave 0: lane j decodes top[j] (token, and whether it is <|endoftext|>); lane 0
+        // walks the K hypotheses in order with the values read back from the lanes
+        const BeamCand cj = top[min(tid, K2 - 1)];
+        const int srcj = cj.i == INT_MAX ? 0 : cj.i / P.V;  // source row
+        const int tokj = cj.i == INT_MAX ? P.eot : cj.i - srcj * P.V;
+        const unsigned cont = (unsigned)__ballot(tid < K2 && tokj != P.eot);  // continuations
+        float cs[KM];
+        int ct[KM];
+#pragma unroll
+        for (int k = 0; k < KM; ++k) {
+            cs[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cj.s), k));
+            ct[k] = __builtin_amdgcn_readlane(tokj, k);
+        }
+        if (tid == 0) {
+            // the last step: max_length, or (length control) the window's token budget
+            const bool is_last = plen + n + 1 >= P.max_length || (budget > 0 && n + 1 >= budget);
+            int sec = K;
+            bool top_fin = false;
+            improved = 0;
+#pragma unroll
+            for (int k = 0; k < KM; ++k) {
+                if (k >= K) break;
+                const int tok = ct[k];
+                int nb = k;
+                if (tok == P.eot || is_last) {
+                    if (k == 0) top_fin = true;
+                    const int len = n + (tok == P.eot ? 0 : 1);
+                    const float norm = len == 0 ? (P.length_penalty != 0.f ? -INFINITY : cs[k])
+                                                : cs[k] / powf((float)len, P.length_penalty);
+                    bw.n_hyp += 1;
+                    if (bw.n_hyp == 1 || norm > bw.best_norm) {
+                        bw.best_norm = norm;
+                        bw.best_raw = cs[k];
+                        bw.best_len = min(len, max_tokens);
+                        best_src = __builtin_amdgcn_readlane(srcj, k);
+                        best_extra = tok == P.eot ? -1 : tok;
+                        improved = 1;
+                    }
+                    // the next continuation at or after position sec replaces it
+                    const unsigned rest = cont & ~((1u << sec) - 1u);
+                    if (rest) {
+                        nb = __ffs(rest) - 1;
+                        sec = nb + 1;
                     }
                 }
+                // row k continues hypothesis nb
+                ch_src[k] = __builtin_amdgcn_readlane(srcj, nb);
+                ch_tok[k] = __builtin_amdgcn_readlane(tokj, nb);
+                ch_score[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cj.s), nb));
             }
-            choose[k] = nb;
+            fin = is_last || (top_fin && bw.n_hyp >= P.num_hyp) || bw.n_hyp >= P.max_cand;
+            bw.done = fin;
+            bwin[w] = bw;
         }
-        fin = is_last || (top_fin && bw.n_hyp >= P.num_hyp) || bw.n_hyp >= P.max_cand;
-        bw.done = fin;
-        bwin[w] = bw;
     }
     __syncthreads();
     OSW_STAMP(7);
@@ -1366,14 +1386,11 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
         }
         return;
     }
-    // row k continues hypothesis top[choose[k]]: its source row's history (positions tid and
-    // tid + 256, both < 448) and ancestry, then the state (thread k)
+    // row k continues hypothesis (ch_src, ch_tok, ch_score)[k]: its source row's history
+    // (positions tid and tid + 256, both < 448) and ancestry, then the state (thread k)
     int qk[KM];
 #pragma unroll
-    for (int k = 0; k < KM; ++k) {
-        const int c = top[choose[min(k, K - 1)]].i;
-        qk[k] = c == INT_MAX ? 0 : c / P.V;
-    }
+    for (int k = 0; k < KM; ++k) qk[k] = ch_src[min(k, K - 1)];
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
         if (k >= K) break;
@@ -1387,16 +1404,14 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
         }
     }
     if (tid < K) {
-        const BeamCand c = top[choose[tid]];
-        const int q = c.i == INT_MAX ? 0 : c.i / P.V;
-        const int tok = c.i == INT_MAX ? P.eot : c.i % P.V;
+        const int q = ch_src[tid], tok = ch_tok[tid];
         if (n < max_tokens) seq[(int64_t)(r0 + tid) * max_tokens + n] = tok;
         SelState s2 = lst[q];
         s2.n_sampled = n + 1;
         s2.penult = s2.last;
         s2.last = tok;
         if (tok >= P.tb) s2.last_ts = tok;
-        s2.sum_lp = c.s;
+        s2.sum_lp = ch_score[tid];
         st[r0 + tid] = s2;
         cur_tok[r0 + tid] = tok;
     }

@@ -793,6 +793,44 @@ constexpr int TOPK_VPT = 16;            // logits one thread holds
 constexpr int MAXK2 = 2 * MAX_BEAM;
 static_assert(BEAM_SLICES * 256 * TOPK_VPT >= SEL_SPLIT * 4096, "osw.hip admits V <= SEL_SPLIT * 4096: one batch per slice");
 
+// Ordered keys for the candidate ranking.  score_key: a float as an int with the same
+// order (-0 as +0, NaN excluded by the callers); an involution, so score_of reads the float
+// back.  rank_key: (score desc, id asc) as one unsigned 64-bit key (0: none).
+// wave_max_key: the wave's largest int in every lane -- row shifts 1, 2, 4, 8 (lane 15 of
+// each row holds the row's maximum), row broadcasts 15 and 31, lane 63 read back.
+__device__ __forceinline__ int score_key(float v) {
+    const int u = __float_as_int(v == 0.f ? 0.f : v);
+    return u ^ ((u >> 31) & 0x7fffffff);
+}
+__device__ __forceinline__ float score_of(int k) { return __int_as_float(k ^ ((k >> 31) & 0x7fffffff)); }
+__device__ __forceinline__ unsigned long long rank_key(float v, int id) {
+    return ((unsigned long long)((unsigned)score_key(v) ^ 0x80000000u) << 32) | (unsigned)~id;
+}
+__device__ __forceinline__ int wave_max_key(int t) {
+    t = max(t, __builtin_amdgcn_update_dpp(INT_MIN, t, 0x111, 0xf, 0xf, false));  // row_shr:1
+    t = max(t, __builtin_amdgcn_update_dpp(INT_MIN, t, 0x112, 0xf, 0xf, false));  // row_shr:2
+    t = max(t, __builtin_amdgcn_update_dpp(INT_MIN, t, 0x114, 0xf, 0xf, false));  // row_shr:4
+    t = max(t, __builtin_amdgcn_update_dpp(INT_MIN, t, 0x118, 0xf, 0xf, false));  // row_shr:8
+    t = max(t, __builtin_amdgcn_update_dpp(INT_MIN, t, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    t = max(t, __builtin_amdgcn_update_dpp(INT_MIN, t, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return __builtin_amdgcn_readlane(t, 63);
+}
+// rank of this lane's key among lanes [0, n) of the wave (n <= 64, wave-uniform; lanes
+// [n, 64) hold key 0, so the walk runs in groups of 4 lanes)
+__device__ __forceinline__ int wave_rank(unsigned long long key, int n) {
+    const unsigned klo = (unsigned)key, khi = (unsigned)(key >> 32);
+    int rank = 0;
+    for (int j = 0; j < n; j += 4) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const unsigned long long f = ((unsigned long long)__builtin_amdgcn_readlane(khi, j + q) << 32) |
+                                         (unsigned)__builtin_amdgcn_readlane(klo, j + q);
+            rank += f > key ? 1 : 0;
+        }
+    }
+    return rank;
+}
+
 // A beam row's sampling step, one vocabulary slice, ONE pass over its logits: the slice
 // statistics of select_partial_body (same entries in the same order, so the same
 // SelPart) and two candidate lists for beam_update: the slice's top 2*beam tokens by raw
@@ -917,19 +955,13 @@ __device__ __forceinline__ void beam_slice_body(const float* __restrict__ logits
 #pragma unroll
         for (int u = 0; u < TOPK_VPT; ++u)
             if ((al >> u) & 1u) lm = fmaxf(lm, xv[u]);
-        ArgMax c{lm, lane};
-        float t = INFINITY;
+        // K2 wave maxima of the lane maxima, each popped lane dropping out (below -inf)
+        int c = score_key(lm), t = INT_MIN;
         for (int r = 0; r < K2; ++r) {
-            ArgMax a = c;
-            auto stp = [&](auto o) {
-                constexpr int O = decltype(o)::value;
-                a = amax(a, ArgMax{xor_lane<O>(a.v), xor_lane<O>(a.i)});
-            };
-            stp(IC<32>{}), stp(IC<16>{}), stp(IC<8>{}), stp(IC<4>{}), stp(IC<2>{}), stp(IC<1>{});
-            t = a.v;
-            if (lane == a.i) c.v = -INFINITY;
+            t = wave_max_key(c);
+            if (lane == __ffsll((long long)__ballot(c == t)) - 1) c = INT_MIN;
         }
-        if (lane == 0) tw[L][tid >> 6] = t;
+        if (lane == 0) tw[L][tid >> 6] = score_of(t);
         if (tid == 0) scnt[L] = 0;
         __syncthreads();
         const float T = fmaxf(fmaxf(tw[L][0], tw[L][1]), fmaxf(tw[L][2], tw[L][3]));
@@ -952,6 +984,14 @@ __device__ __forceinline__ void beam_slice_body(const float* __restrict__ logits
         __syncthreads();
         const int n = scnt[L];
         if (n > SCAP) return false;
+        if (n <= 64) {  // wave 0, one member per lane
+            if (tid < 64) {
+                const BeamCand e = sset[L][min(tid, n - 1)];
+                const int rank = wave_rank(tid < n ? rank_key(e.s, e.i) : 0ull, n);
+                if (tid < n && rank < K2) out[rank] = e;
+            }
+            return true;
+        }
         for (int i = tid; i < n; i += 256) {
             const BeamCand e = sset[L][i];
             int rank = 0;
@@ -1232,8 +1272,7 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
                 const float v = rsum[k] + (c.s - rlse[k]);
                 if (c.i != INT_MAX && !(first && k != 0) && !(v != v)) {
                     cx[j] = k * P.V + c.i;
-                    const int u = __float_as_int(v == 0.f ? 0.f : v);
-                    ck[j] = u ^ ((u >> 31) & 0x7fffffff);
+                    ck[j] = score_key(v);
                 }
             }
         }
@@ -1250,16 +1289,7 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
                 ck[b - 1] = sw ? tk : ck[b - 1];
             }
         for (int r = 0; r < K2; ++r) {
-            // wave maximum into lane 63: row shifts 1, 2, 4, 8 (lane 15 of each row holds the
-            // row's maximum), then row broadcasts 15 and 31 (lanes without a source see INT_MIN)
-            int t = ck[0];
-            t = max(t, __builtin_amdgcn_update_dpp(INT_MIN, t, 0x111, 0xf, 0xf, false));  // row_shr:1
-            t = max(t, __builtin_amdgcn_update_dpp(INT_MIN, t, 0x112, 0xf, 0xf, false));  // row_shr:2
-            t = max(t, __builtin_amdgcn_update_dpp(INT_MIN, t, 0x114, 0xf, 0xf, false));  // row_shr:4
-            t = max(t, __builtin_amdgcn_update_dpp(INT_MIN, t, 0x118, 0xf, 0xf, false));  // row_shr:8
-            t = max(t, __builtin_amdgcn_update_dpp(INT_MIN, t, 0x142, 0xa, 0xf, false));  // row_bcast:15
-            t = max(t, __builtin_amdgcn_update_dpp(INT_MIN, t, 0x143, 0xc, 0xf, false));  // row_bcast:31
-            const int m = __builtin_amdgcn_readlane(t, 63);
+            const int m = wave_max_key(ck[0]);
             const unsigned long long tie = __ballot(ck[0] == m);
             int owner = __ffsll((long long)tie) - 1;
             if (__popcll(tie) > 1) {  // equal scores: the smallest flat id
@@ -1273,7 +1303,7 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
                 owner = __ffsll((long long)__ballot(ck[0] == m && cx[0] == im)) - 1;
             }
             if (lane == 0)
-                wtop[wv * K2 + r] = ArgMax{__int_as_float(m ^ ((m >> 31) & 0x7fffffff)),
+                wtop[wv * K2 + r] = ArgMax{score_of(m),
                                            __builtin_amdgcn_readlane(cx[0], owner)};
             if (lane == owner) {
 #pragma unroll
@@ -1292,21 +1322,7 @@ __device__ __forceinline__ void beam_update_body(const SelParams& P, const int* 
             const int S = 4 * K2;  // <= 64 (K2 <= 2 * KM <= 16)
             const ArgMax e = lane < S ? wtop[lane] : ArgMax{-INFINITY, INT_MAX};
             const bool valid = lane < S && e.i != INT_MAX;
-            // rank = #survivors before e in amax order, by one unsigned 64-bit key per
-            // survivor (ordered score, then ~id; 0 for none)
-            const int u = __float_as_int(e.v == 0.f ? 0.f : e.v);
-            const unsigned long long key =
-                valid ? ((unsigned long long)((unsigned)(u ^ ((u >> 31) & 0x7fffffff)) ^ 0x80000000u) << 32) |
-                            (unsigned)~e.i
-                      : 0ull;
-            const unsigned klo = (unsigned)key, khi = (unsigned)(key >> 32);
-            int rank = 0;
-#pragma unroll 4
-            for (int j = 0; j < S; ++j) {
-                const unsigned long long f = ((unsigned long long)__builtin_amdgcn_readlane(khi, j) << 32) |
-                                             (unsigned)__builtin_amdgcn_readlane(klo, j);
-                rank += f > key ? 1 : 0;
-            }
+            const int rank = wave_rank(valid ? rank_key(e.v, e.i) : 0ull, S);
             const int nvalid = __popcll(__ballot(valid));
             if (valid && rank < K2) top[rank] = BeamCand{e.v, e.i};
             if (lane < K2 && lane >= nvalid) top[lane] = BeamCand{-INFINITY, INT_MAX};

@@ -767,7 +767,7 @@ __global__ __launch_bounds__(256) void dec_xattn_mfma_kernel(const float* __rest
 __global__ __launch_bounds__(256) void dec_resid_ln_kernel(ResLnArgs A, h16* __restrict__ y, int64_t lo_off) {
     __shared__ __attribute__((aligned(16))) float red[resln_scratch(1, 1280)];
     const int b = blockIdx.x;
-    resln_rows<1, 8>(A, b, 1, true, red,
+    resln_rows<1, 8, true>(A, b, 1, true, red,
                   [&](int, int c, float v) { split_h16(v, y, y + lo_off, (int64_t)b * A.D + c); });
 }
 

@@ -1455,8 +1455,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL ? 4 : 1
         // (the fused-selection logits GEMM: 10 per batch, two round trips for fc2's 20 slabs,
         // so its VGPRs fit 4 workgroups per CU and its 811 workgroups run in one round)
         constexpr int KBIG = SEL ? 8 : 24;
-        if (pa.ln.ks <= 8) resln_rows<PRO_ROWS, 8>(pa.ln, 0, g.M, wx, pred, put);
-        else resln_rows<PRO_ROWS, KBIG>(pa.ln, 0, g.M, wx, pred, put);
+        // (early residual loads where the VGPRs allow: not in the selecting logits GEMM, not
+        // beside 24 slabs)
+        if (pa.ln.ks <= 8) resln_rows<PRO_ROWS, 8, !SEL>(pa.ln, 0, g.M, wx, pred, put);
+        else resln_rows<PRO_ROWS, KBIG, false>(pa.ln, 0, g.M, wx, pred, put);
         __syncthreads();
     } else if constexpr (PRO == PRO_GELU) {
         const int64_t slab = (int64_t)g.M * g.K;

@@ -8,8 +8,8 @@
 //             y  = (x' - mean) * rstd * g + b   (two-pass variance, eps 1e-5, fp32)
 // 256 threads; thread t owns columns 4t..4t+3 (one 16-B piece) and 1024 + t (D <= 1280).
 // Every slab piece of a row is loaded before any is added (8 slabs per batch, clamped
-// addresses, the surplus added as exact zeros), so a row costs one memory round trip
-// per 8 slabs; the sums run in slab order, the thread's 5 columns in order, then
+// addresses, the surplus added as exact zeros), with the residual, bias, gain and shift
+// issued ahead of the first batch, so a row costs one memory round trip per 8 slabs; the sums run in slab order, the thread's 5 columns in order, then
 // wave_sum, then the 4 wave partials in order.
 #pragma once
 #include "common.h"
@@ -38,14 +38,43 @@ struct ResLnArgs {
 
 // rows r0 .. r0+nr-1 (nr <= NR); emit(r, c, y) receives every LayerNorm output;
 // write_x: this workgroup stores x'.  red: LDS scratch of 2 * NR * 4 floats.  KB: slab
-// loads per batch (the sums do not depend on it: the padding adds exact zeros).
-template <int NR, int KB, class Emit>
+// loads per batch (the sums do not depend on it: the padding adds exact zeros).  EARLY:
+// the residual, bias, gain and shift are loaded ahead of the first slab batch (one round
+// trip fewer, ~15 more VGPRs); otherwise after the slabs / the statistics.  Same arithmetic.
+template <int NR, int KB, bool EARLY, class Emit>
 __device__ __forceinline__ void resln_rows(const ResLnArgs& A, int r0, int nr, bool write_x, float* red, Emit emit) {
 #pragma clang fp contract(off)
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
     const int D = A.D;
     const bool h4 = 4 * t < D, h1 = 1024 + t < D;
     const int c4 = h4 ? 4 * t : 0, c1 = h1 ? 1024 + t : 0;  // clamped: every load stays in the row
+    // issued before the first slab batch, so they share its round trip: the LayerNorm gain
+    // and shift, the bias, every row's residual (all rows' loads precede any x' store, so
+    // x_out aliasing x_in is harmless)
+    f32x4 g4, b4, bias4 = {0.f, 0.f, 0.f, 0.f}, x4[NR];
+    float g1, b1, bias1 = 0.f, x1[NR];
+    auto load_gb = [&]() {
+        g4 = *(const f32x4*)(A.g + c4);
+        b4 = *(const f32x4*)(A.b + c4);
+        g1 = A.g[c1];
+        b1 = A.b[c1];
+    };
+    auto load_x = [&]() {
+        if (A.bias) {
+            bias4 = *(const f32x4*)(A.bias + c4);
+            bias1 = A.bias[c1];
+        }
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const int64_t rb = (int64_t)(r0 + min(r, nr - 1)) * D;
+            x4[r] = *(const f32x4*)(A.x_in + rb + c4);
+            x1[r] = A.x_in[rb + c1];
+        }
+    };
+    if constexpr (EARLY) {
+        load_gb();
+        if (A.part) load_x();
+    }
     float v[NR][5];
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
@@ -74,11 +103,13 @@ __device__ __forceinline__ void resln_rows(const ResLnArgs& A, int r0, int nr, b
                     s1 += in ? p1[j] : 0.f;
                 }
             }
-            a4 = *(const f32x4*)(A.x_in + rb + c4);
-            a1 = A.x_in[rb + c1];
+            if constexpr (!EARLY)
+                if (r == 0) load_x();
+            a4 = x4[r];
+            a1 = x1[r];
             if (A.bias) {
-                a4 += *(const f32x4*)(A.bias + c4);
-                a1 += A.bias[c1];
+                a4 += bias4;
+                a1 += bias1;
             }
             a4 += s4;
             a1 += s1;
@@ -132,8 +163,7 @@ __device__ __forceinline__ void resln_rows(const ResLnArgs& A, int r0, int nr, b
                          red[(NR + r) * 4 + 3]);
         rstd[r] = rsqrtf(q / D + 1e-5f);
     }
-    const f32x4 g4 = *(const f32x4*)(A.g + c4), b4 = *(const f32x4*)(A.b + c4);
-    const float g1 = A.g[c1], b1 = A.b[c1];
+    if constexpr (!EARLY) load_gb();
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
         if (r >= nr) break;

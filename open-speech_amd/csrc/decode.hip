@@ -184,22 +184,55 @@ __device__ __forceinline__ void reduce_head(const float* __restrict__ part, int 
 // (t / 64) and reproduces reduce_head's summation order exactly (per-wave slab sums
 // s = w, w+4, ... then bias + (((w0 + w1) + w2) + w3)), so the result is bit-identical
 // to three reduce_head calls, in one round trip and one barrier instead of three and six.
-__device__ __forceinline__ void reduce_qkv(const float* __restrict__ part, int ks, int64_t slab, int64_t row, int D,
-                                           int h, const float* __restrict__ bias, h16* q16, h16* kdst, h16* vdst) {
+// q/k/v element t (< 3 * HD) of head h: bias + the split-K slabs summed as four chains
+// (chain w: slabs w, w+4 pairwise by 8, then the chains in order).  QkvLoad issues every
+// load up front (ks <= 16: one round trip; clamped addresses, the surplus unused) so the
+// kernel can test the row's state meanwhile; qkv_finish sums in the same order for any ks.
+struct QkvLoad {
+    float p[16];
+    float bias;
+};
+__device__ __forceinline__ void qkv_load(const float* __restrict__ part, int ks, int64_t slab, int64_t row, int D,
+                                         int h, const float* __restrict__ bias, QkvLoad& L) {
+    const int t = threadIdx.x;
+    if (t < 3 * HD) {
+        const int which = t >> 6, d = t & 63;
+        const int64_t off = row + which * D + h * HD + d;
+        L.bias = bias[which * D + h * HD + d];
+        if (ks <= 16) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) L.p[j] = part[min(j, ks - 1) * slab + off];
+        }
+    }
+}
+__device__ __forceinline__ void qkv_finish(const float* __restrict__ part, int ks, int64_t slab, int64_t row, int D,
+                                           int h, const QkvLoad& L, h16* q16, h16* kdst, h16* vdst) {
     const int t = threadIdx.x;
     if (t < 3 * HD) {
         const int which = t >> 6, d = t & 63;
         const int64_t off = row + which * D + h * HD + d;
         float ws[4];
+        if (ks <= 16) {
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            float v = 0.f;
-            int s = w;
-            for (; s + 4 < ks; s += 8) v += part[s * slab + off] + part[(s + 4) * slab + off];
-            if (s < ks) v += part[s * slab + off];
-            ws[w] = v;
+            for (int w = 0; w < 4; ++w) {
+                float v = 0.f;
+                if (w + 4 < ks) v += L.p[w] + L.p[w + 4];
+                else if (w < ks) v += L.p[w];
+                if (w + 12 < ks) v += L.p[w + 8] + L.p[w + 12];
+                else if (w + 8 < ks) v += L.p[w + 8];
+                ws[w] = v;
+            }
+        } else {
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                float v = 0.f;
+                int s = w;
+                for (; s + 4 < ks; s += 8) v += part[s * slab + off] + part[(s + 4) * slab + off];
+                if (s < ks) v += part[s * slab + off];
+                ws[w] = v;
+            }
         }
-        float r = bias[which * D + h * HD + d];
+        float r = L.bias;
         r += ws[0] + ws[1] + ws[2] + ws[3];
         h16* dst = which == 0 ? q16 : which == 1 ? kdst : vdst;
         dst[d] = (h16)r;
@@ -233,16 +266,14 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
         h = blockIdx.x % H;
         b = blockIdx.x / H;
     }
-    // a finished row (its <|endoftext|> is chosen; graph replays keep stepping it until
-    // the whole batch is done) reads and writes nothing: its outputs are never used
-    if (st[b].done) return;
+    // every load of the prologue in one round trip: the row's state and position, its
+    // ancestry (GATHER), the q/k/v slabs and bias
+    const int done = st[b].done;
     const int D = H * HD;
     // graph replays may run past max_length on finished windows; pos_row: per-row counters (row refill)
     const int pos = min(pos_ptr[pos_row ? b : 0], ctx - 1);
-    h16* kc = kcache + ((int64_t)b * H + h) * ctx * HD;
-    h16* vc = vcache + ((int64_t)b * H + h) * ctx * HD;
     __shared__ int soff[GATHER ? 512 : 1];
-    int an2[2];  // ancestry of keys tid and tid + 256 (ctx <= 448 < 512), issued before the slab loads
+    int an2[2];  // ancestry of keys tid and tid + 256 (ctx <= 448 < 512)
     if constexpr (GATHER) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -251,7 +282,14 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
         }
     }
     const int64_t slab = (int64_t)B * 3 * D, row = (int64_t)b * 3 * D;
-    reduce_qkv(part, ks, slab, row, D, h, bias, q16, kc + (int64_t)pos * HD, vc + (int64_t)pos * HD);
+    QkvLoad L;
+    qkv_load(part, ks, slab, row, D, h, bias, L);
+    // a finished row (its <|endoftext|> is chosen; graph replays keep stepping it until
+    // the whole batch is done) writes nothing and reads nothing more: its outputs are never used
+    if (done) return;
+    h16* kc = kcache + ((int64_t)b * H + h) * ctx * HD;
+    h16* vc = vcache + ((int64_t)b * H + h) * ctx * HD;
+    qkv_finish(part, ks, slab, row, D, h, L, q16, kc + (int64_t)pos * HD, vc + (int64_t)pos * HD);
     if constexpr (GATHER) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {

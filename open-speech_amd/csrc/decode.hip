@@ -419,6 +419,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
     const int per = (T + XCH - 1) / XCH;
     const int k0 = chunk * per, nk = min(T, k0 + per) - k0;
     const int64_t hoff = ((int64_t)w * H + h) * T * HD;
+    // q of row r0 + k: fp16(bias + Σ split-K partials) / sqrt(64), the order of reduce_head
+    // (wave wv: slabs wv, wv+4 pairwise by 8).  With ks <= 8 the wave's two slabs and the
+    // bias are issued before the K/V stream, so the q reduction waits for them alone.
+    const int r0 = w * beam;
+    const int64_t slab = (int64_t)W * beam * D;
+    const float bq = bias[h * HD + lane];
+    float qa[NB], qb[NB];
+    if (ks <= 8) {
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            const int64_t off = (int64_t)(r0 + min(k, beam - 1)) * D + h * HD + lane;
+            qa[k] = part[min(wv, ks - 1) * slab + off];
+            qb[k] = part[min(wv + 4, ks - 1) * slab + off];
+        }
+    }
     h16x8 kf[XU], vf[XU];
 #pragma unroll
     for (int u = 0; u < XU; ++u) {
@@ -426,17 +441,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
         kf[u] = __builtin_nontemporal_load((const h16x8*)(xk + hoff + (int64_t)key * HD + 8 * c));
         vf[u] = __builtin_nontemporal_load((const h16x8*)(xv + hoff + (int64_t)key * HD + 8 * c));
     }
-    // q of row r0 + k: fp16(bias + Σ split-K partials) / sqrt(64), the order of reduce_head
-    const int r0 = w * beam;
-    const int64_t slab = (int64_t)W * beam * D;
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
         if (k >= beam) break;
-        const int64_t off = (int64_t)(r0 + k) * D + h * HD + lane;
         float v = 0.f;
-        int s = wv;
-        for (; s + 4 < ks; s += 8) v += part[s * slab + off] + part[(s + 4) * slab + off];
-        if (s < ks) v += part[s * slab + off];
+        if (ks <= 8) {
+            if (wv + 4 < ks) v += qa[k] + qb[k];
+            else if (wv < ks) v += qa[k];
+        } else {
+            const int64_t off = (int64_t)(r0 + k) * D + h * HD + lane;
+            int s = wv;
+            for (; s + 4 < ks; s += 8) v += part[s * slab + off] + part[(s + 4) * slab + off];
+            if (s < ks) v += part[s * slab + off];
+        }
         red[wv][k][lane] = v;
     }
     __syncthreads();
@@ -444,7 +461,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NB > 5 ? 4 
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
             if (k >= beam) break;
-            float r = bias[h * HD + lane];
+            float r = bq;
             r += red[0][k][lane] + red[1][k][lane] + red[2][k][lane] + red[3][k][lane];
             qsh[k][lane] = (float)(h16)r * 0.125f;
         }

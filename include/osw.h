@@ -33,6 +33,26 @@
  * caller-owned and only read/written during the call (the library copies them).
  * A context serialises its own calls (internal mutex); one context per device.
  * No torch types cross this boundary.
+ *
+ * Concurrency contract (the reference calls transcribe from several executor pools at
+ * once, src/main.py:305, src/streaming.py:50-52, src/realtime/server.py:33-35, and loads
+ * models on demand while serving, src/backends/faster_whisper.py:210-215):
+ *   - any entry point may be called from any thread, on any context, at any time: calls
+ *     on one context run one at a time; calls on different contexts (sibling lanes of
+ *     one GPU, other GPUs, other models) run concurrently;
+ *   - a context's decode steps are captured into hipGraphs on first use.  No entry point
+ *     touches the legacy (null) stream: copies and memsets run on the context's own
+ *     non-blocking stream.  Entry points that allocate, free, create or destroy streams
+ *     (osw_create, osw_create_sibling, osw_destroy, osw_set_weight, osw_get_mel,
+ *     osw_debug_gemm, a call whose input outgrows the resident buffers, the first ingest
+ *     call on a device) wait for a capture in progress to end (one process-wide capture
+ *     gate), so none of them can invalidate another context's capture;
+ *   - the caller's own HIP / torch work in the same process must stay off the legacy
+ *     stream while contexts are serving (e.g. run torch on a torch.cuda.Stream, which is
+ *     non-blocking): HIP refuses legacy-stream work while any stream of the process
+ *     captures, and the library cannot see it;
+ *   - OSW_ECAPTURE reports a refused or invalidated stream capture: the context and the
+ *     device remain usable, the call may be retried (it is not a device fault).
  */
 #ifndef OSW_H
 #define OSW_H
@@ -48,6 +68,7 @@ extern "C" {
 #define OSW_ENOMEM (-12)
 #define OSW_EHIP (-100)
 #define OSW_ESTATE (-101)
+#define OSW_ECAPTURE (-102)
 
 typedef struct osw_ctx osw_ctx;
 
@@ -239,6 +260,11 @@ int osw_encoder_layer_debug(osw_ctx* ctx, int32_t layer, const float* x, float* 
  * runs `iters` times and stores the mean kernel time (ms, HIP events) in *ms. */
 int osw_debug_gemm(osw_ctx* ctx, int32_t M, int32_t N, int32_t K, int32_t variant, const void* A, const void* W,
                    float* C, int32_t iters, float* ms);
+
+/* Test hook for the concurrency contract: holds a stream capture open on the context's
+ * stream for hold_ms (under the same locks as a decode-graph capture) and fails if it was
+ * invalidated meanwhile.  Other threads' calls run during the hold. */
+int osw_debug_hold_capture(osw_ctx* ctx, int32_t hold_ms);
 
 /* 0 off; 1 per-stage HIP-event timers (decode steps stay in their hipGraph, so only
  * mel / encoder stages are timed); 2 also launches the decode steps eagerly so the

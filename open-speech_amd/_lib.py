@@ -92,6 +92,7 @@ _SIGS = {
     "osw_encoder_layer_debug": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_float), P(C.c_float), C.c_int32]),
     "osw_debug_gemm": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
                                  P(C.c_float), C.c_int32, P(C.c_float)]),
+    "osw_debug_hold_capture": (C.c_int, [C.c_void_p, C.c_int32]),
     "osw_set_encoder_baton_min": (C.c_int, [C.c_void_p, C.c_int32]),
     "osw_set_profiling": (C.c_int, [C.c_void_p, C.c_int32]),
     "osw_get_profile": (C.c_int, [C.c_void_p, P(osw_profile)]),
@@ -127,6 +128,7 @@ def load() -> C.CDLL:
 
 
 OSW_EHIP = -100
+OSW_ECAPTURE = -102
 
 
 class OswError(RuntimeError):
@@ -141,8 +143,13 @@ class OswDeviceError(OswError):
     """OSW_EHIP: a HIP runtime error on the context's device (the batcher fails the GPU over)."""
 
 
+class OswCaptureError(OswError):
+    """OSW_ECAPTURE: a stream capture was refused or invalidated.  Not a device fault: the
+    context and the GPU stay usable (the batcher fails only the affected requests)."""
+
+
 def check(rc: int, what: str = "") -> None:
     if rc != OSW_OK:
         msg = load().osw_last_error().decode(errors="replace")
-        cls = OswDeviceError if rc == OSW_EHIP else OswError
+        cls = {OSW_EHIP: OswDeviceError, OSW_ECAPTURE: OswCaptureError}.get(rc, OswError)
         raise cls(f"{what} failed ({rc}): {msg}", rc)

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -20,6 +21,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/osw.h"
@@ -60,12 +62,31 @@ struct OswError : std::runtime_error {
     OswError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
 };
 
+// Stream-capture errors are refusals of an operation, not device faults: the context and
+// the GPU stay usable, so they get their own code (OSW_ECAPTURE) and the serving layer does
+// not fail the GPU over on them (runner.py).
+inline int hip_code(hipError_t e) {
+    switch (e) {
+        case hipErrorStreamCaptureUnsupported:
+        case hipErrorStreamCaptureInvalidated:
+        case hipErrorStreamCaptureMerge:
+        case hipErrorStreamCaptureUnmatched:
+        case hipErrorStreamCaptureUnjoined:
+        case hipErrorStreamCaptureIsolation:
+        case hipErrorStreamCaptureImplicit:
+        case hipErrorCapturedEvent:
+        case hipErrorStreamCaptureWrongThread:
+            return OSW_ECAPTURE;
+        default:
+            return OSW_EHIP;
+    }
+}
 #define HIPCHK(x)                                                                                  \
     do {                                                                                           \
         hipError_t e_ = (x);                                                                       \
         if (e_ != hipSuccess)                                                                      \
-            throw OswError(OSW_EHIP, std::string(#x) + ": " + hipGetErrorString(e_) + " @" +       \
-                                         std::to_string(__LINE__));                                \
+            throw OswError(hip_code(e_), std::string(#x) + ": " + hipGetErrorString(e_) + " @" +   \
+                                             std::to_string(__LINE__));                            \
     } while (0)
 #define REQUIRE(c, msg) \
     do {                \
@@ -99,8 +120,29 @@ struct Tensor {
     int frag_n = 0, frag_k = 0;
 };
 
+// The capture gate (one per process).  While a stream is being captured into a hipGraph,
+// HIP refuses every operation that would make the legacy (null) stream depend on it
+// ("operation would make the legacy stream depend on a capturing blocking stream") and
+// invalidates the capture; its capture-status check spans every stream of the process, so
+// a synchronous hipMemcpy / hipMemset, hipMalloc / hipFree, hipDeviceSynchronize or stream
+// creation on one lane's thread breaks a sibling lane's capture (GPUTEST_r05).  So:
+//   * a decode graph is captured only while holding this gate (decode_graph);
+//   * every allocation, free, stream / pinned-buffer creation or destruction and every
+//     implicitly synchronising call takes it too (dalloc / dfree, osw_create,
+//     osw_create_sibling, osw_destroy, osw_set_weight, osw_get_mel, osw_debug_gemm, ingest);
+//   * everything else a call does runs on the context's own non-blocking stream
+//     (hipMemcpyAsync / hipMemsetAsync + hipStreamSynchronize), never on the legacy stream.
+// Recursive: osw_create holds it across setup_workspace's dalloc calls.  Lock order: a
+// context's mu, then the encoder baton's mu, then this gate; nothing is locked under it.
+std::recursive_mutex& capture_gate() {
+    static std::recursive_mutex m;
+    return m;
+}
+using GateLock = std::lock_guard<std::recursive_mutex>;
+
 template <typename T>
 T* dalloc(size_t n, std::vector<void*>& owned) {
+    GateLock gate_(capture_gate());
     void* p = nullptr;
     if (n == 0) n = 1;
     hipError_t e = hipMalloc(&p, n * sizeof(T));
@@ -118,6 +160,7 @@ void dfree(T*& p, std::vector<void*>& owned) {
             owned.erase(it);
             break;
         }
+    GateLock gate_(capture_gate());
     (void)hipFree(p);
     p = nullptr;
 }
@@ -417,10 +460,12 @@ void build_weight_table(osw_ctx* c) {
     size_t total = 0;
     for (auto& kv : c->w) total += ((size_t)kv.second.numel * (kv.second.f16 ? 2 : 4) + 255) & ~(size_t)255;
     void* ap = nullptr;
+    GateLock gate_(capture_gate());
     if (hipMalloc(&ap, total) != hipSuccess)
         throw OswError(OSW_ENOMEM, "hipMalloc " + std::to_string(total) + " B (weights) failed");
     const int dev = c->device;
     c->arena = std::shared_ptr<void>(ap, [dev](void* p) {
+        GateLock gate_(capture_gate());
         int prev = -1;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(dev);
@@ -504,18 +549,20 @@ void setup_mel(osw_ctx* c) {
         off[m] = (int)wts.size();
         for (int k = first; k <= last; ++k) wts.push_back(row[k]);
     }
+    // (the host vectors live until the copies are done: synchronised before returning)
     c->tw400 = dalloc<float2>(400, c->owned);
     c->hann = dalloc<float>(400, c->owned);
     c->flo = dalloc<int>(n_mels, c->owned);
     c->fcnt = dalloc<int>(n_mels, c->owned);
     c->foff = dalloc<int>(n_mels, c->owned);
     c->fw = dalloc<float>(wts.size(), c->owned);
-    HIPCHK(hipMemcpy(c->tw400, tw.data(), 400 * sizeof(float2), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->hann, hn.data(), 400 * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->flo, lo.data(), n_mels * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->fcnt, cnt.data(), n_mels * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->foff, off.data(), n_mels * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->fw, wts.data(), wts.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpyAsync(c->tw400, tw.data(), 400 * sizeof(float2), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->hann, hn.data(), 400 * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->flo, lo.data(), n_mels * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->fcnt, cnt.data(), n_mels * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->foff, off.data(), n_mels * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->fw, wts.data(), wts.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
 }
 
 void setup_workspace(osw_ctx* c) {
@@ -526,7 +573,7 @@ void setup_workspace(osw_ctx* c) {
     c->win = dalloc<int>(3 * B, o);
     c->X1 = dalloc<h16>(B * 3002 * c->C1, o);
     c->H1 = dalloc<h16>(B * 3001 * De, o);
-    HIPCHK(hipMemset(c->H1, 0, (size_t)B * 3001 * De * 2));  // row 0 of every window stays zero
+    HIPCHK(hipMemsetAsync(c->H1, 0, (size_t)B * 3001 * De * 2, c->stream));  // row 0 of every window stays zero
     c->X = dalloc<float>(Me * De, o);
     c->Xn = dalloc<h16>(Me * De, o);
     c->QKV = dalloc<h16>(3 * Me * De, o);
@@ -563,11 +610,11 @@ void setup_workspace(osw_ctx* c) {
     c->bcand = dalloc<char>((size_t)R * beam_cand_bytes(MAX_BEAM), o);
     c->xws = dalloc<float>(R * d.n_text_head * XCHUNKS * XPART, o);
     c->xticket = dalloc<int>(B * d.n_text_head, o);
-    HIPCHK(hipMemset(c->xticket, 0, (size_t)B * d.n_text_head * sizeof(int)));
+    HIPCHK(hipMemsetAsync(c->xticket, 0, (size_t)B * d.n_text_head * sizeof(int), c->stream));
     c->budget = dalloc<int>(R, o);
     c->seed_d = dalloc<unsigned long long>(1, o);
     c->sel_arrive = dalloc<int>(1 + R, o);  // [0] rows finalised, [1 + row] slice tickets
-    HIPCHK(hipMemset(c->sel_arrive, 0, (1 + (size_t)R) * sizeof(int)));
+    HIPCHK(hipMemsetAsync(c->sel_arrive, 0, (1 + (size_t)R) * sizeof(int), c->stream));
     {
         const int64_t shapes[][2] = {{3 * Dd, Dd}, {Dd, Dd}, {4 * Dd, Dd}, {Dd, 4 * Dd}, {d.n_vocab, Dd}};
         for (auto& nk : shapes)  // skinny split-K slabs: decoder projections at any row count
@@ -584,6 +631,7 @@ void setup_workspace(osw_ctx* c) {
             if (nk[0] != d.n_vocab) p2 = std::max<int64_t>(p2, (int64_t)skinny_ksplit((int)nk[0], (int)nk[1]) * nk[0]);
         c->part2 = dalloc<float>(p2 * std::min<int64_t>(R, GELU_ROWS), o);
     }
+    GateLock gate_(capture_gate());
     HIPCHK(hipHostMalloc((void**)&c->done_host, sizeof(int), 0));
 }
 
@@ -941,6 +989,15 @@ hipGraphExec_t decode_graph(osw_ctx* c, const std::vector<int64_t>& key, const s
     }
     {
         constexpr size_t kMaxGraphs = 16;
+        // A sibling lane's encoder waits on the baton event, which this lane may have
+        // recorded on this stream: HIP refuses that wait while this stream captures
+        // ("dependency created on uncaptured work in another stream"), so no sibling
+        // enqueues an encoder (which holds the baton's mutex) during a capture.  And no
+        // thread of the process touches the legacy stream or synchronises implicitly while
+        // it captures: the capture gate (capture_gate) is held from here to the instantiation.
+        std::unique_lock<std::mutex> no_encoder;
+        if (c->baton) no_encoder = std::unique_lock<std::mutex>(c->baton->mu);
+        GateLock gate_(capture_gate());
         if (c->dgraphs.size() >= kMaxGraphs) {  // evict the least recently used
             auto lru = c->dgraphs.begin();
             for (auto it = c->dgraphs.begin(); it != c->dgraphs.end(); ++it)
@@ -953,12 +1010,6 @@ hipGraphExec_t decode_graph(osw_ctx* c, const std::vector<int64_t>& key, const s
         HIPCHK(hipStreamSynchronize(c->stream));
         hipGraph_t gr = nullptr;
         hipGraphExec_t ge = nullptr;
-        // A sibling lane's encoder waits on the baton event, which this lane may have
-        // recorded on this stream: HIP refuses that wait while this stream captures
-        // ("dependency created on uncaptured work in another stream"), so no sibling
-        // enqueues an encoder (which holds the baton's mutex) during a capture.
-        std::unique_lock<std::mutex> no_encoder;
-        if (c->baton) no_encoder = std::unique_lock<std::mutex>(c->baton->mu);
         c->capturing = true;
         try {
             trace_graph(c, "capture begin");
@@ -1391,6 +1442,7 @@ IngestDev& ingest_dev(int device) {
         REQUIRE(device >= 0 && device < ndev, "device ordinal out of range");
         p.reset(new IngestDev());
         DeviceScope dev_scope_((device));
+        GateLock gate_(capture_gate());
         HIPCHK(hipStreamCreateWithFlags(&p->s, hipStreamNonBlocking));
         p->leaves = dalloc<int2>(128, p->owned);
     }
@@ -1760,6 +1812,7 @@ int osw_create(const osw_dims* dims, int32_t device, int32_t max_batch, osw_ctx*
         int ndev = 0;
         HIPCHK(hipGetDeviceCount(&ndev));
         REQUIRE(device >= 0 && device < ndev, "device ordinal out of range");
+        GateLock gate_(capture_gate());  // streams, allocations, kernel attributes
         c = new osw_ctx();
         c->device = device;
         c->d = *dims;
@@ -1781,10 +1834,10 @@ int osw_create(const osw_dims* dims, int32_t device, int32_t max_batch, osw_ctx*
         setup_mel(c);
         setup_workspace(c);
         HIPCHK(hipStreamSynchronize(c->stream));
-        HIPCHK(hipDeviceSynchronize());
         *out = c;
     });
     if (rc != OSW_OK && c) {
+        GateLock gate_(capture_gate());
         for (void* p : c->owned) (void)hipFree(p);
         destroy_streams(c);
         delete c;
@@ -1799,6 +1852,7 @@ int osw_create_sibling(osw_ctx* parent, int32_t max_batch, osw_ctx** out) {
         REQUIRE(max_batch >= 1 && max_batch <= 1024, "max_batch out of range");
         std::lock_guard<std::mutex> lk(parent->mu);
         REQUIRE(parent->finalized, "parent context weights not finalized");
+        GateLock gate_(capture_gate());
         c = new osw_ctx();
         c->device = parent->device;
         c->d = parent->d;
@@ -1820,6 +1874,7 @@ int osw_create_sibling(osw_ctx* parent, int32_t max_batch, osw_ctx** out) {
         *out = c;
     });
     if (rc != OSW_OK && c) {
+        GateLock gate_(capture_gate());
         for (void* p : c->owned) (void)hipFree(p);
         destroy_streams(c);
         delete c;
@@ -1834,6 +1889,7 @@ int osw_destroy(osw_ctx* c) {
             std::lock_guard<std::mutex> lk(c->mu);
             DeviceScope dev_scope_((c->device));
             HIPCHK(hipStreamSynchronize(c->stream));
+            GateLock gate_(capture_gate());
             for (auto& e : c->evs) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
             for (auto e : c->ev_free) (void)hipEventDestroy(e);
             for (auto& kv : c->dgraphs) (void)hipGraphExecDestroy(kv.second.first);
@@ -1854,6 +1910,7 @@ int osw_set_weight(osw_ctx* c, const char* name, const void* host, int64_t nbyte
         std::lock_guard<std::mutex> lk(c->mu);
         REQUIRE(!c->sibling, "sibling contexts share their parent's weights (read-only)");
         DeviceScope dev_scope_((c->device));
+        GateLock gate_(capture_gate());  // weight upload (a model loading while another serves)
         Tensor& t = W(c, name);
         const std::string nm(name);
         if (nm == "enc.conv1.w" && c->C1 != c->d.n_mels) {
@@ -1864,10 +1921,11 @@ int osw_set_weight(osw_ctx* c, const char* name, const void* host, int64_t nbyte
             for (int64_t o = 0; o < De; ++o)
                 for (int k = 0; k < 3; ++k)
                     std::memcpy(&pad[(o * 3 + k) * c->C1], &src[(o * 3 + k) * M], M * 2);
-            HIPCHK(hipMemcpy(t.ptr, pad.data(), pad.size() * 2, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpyAsync(t.ptr, pad.data(), pad.size() * 2, hipMemcpyHostToDevice, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));  // before `pad` goes
         } else {
             REQUIRE(nbytes == t.numel * (t.f16 ? 2 : 4), "tensor " + nm + ": wrong byte count");
-            HIPCHK(hipMemcpy(t.ptr, host, nbytes, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpyAsync(t.ptr, host, nbytes, hipMemcpyHostToDevice, c->stream));
         }
         pack_frag(c, nm);
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -1882,8 +1940,8 @@ int osw_get_weight(osw_ctx* c, const char* name, void* host, int64_t nbytes) {
         DeviceScope dev_scope_((c->device));
         Tensor& t = W(c, name);
         REQUIRE(nbytes == t.numel * (t.f16 ? 2 : 4), std::string("tensor ") + name + ": wrong byte count");
+        HIPCHK(hipMemcpyAsync(host, t.ptr, nbytes, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
-        HIPCHK(hipMemcpy(host, t.ptr, nbytes, hipMemcpyDeviceToHost));
     });
 }
 
@@ -1939,12 +1997,12 @@ int osw_get_mel(osw_ctx* c, int32_t clip, float* out, int64_t out_floats) {
         const int nf = c->nframes[clip];
         const int64_t n = (int64_t)nf * c->d.n_mels;
         REQUIRE(out_floats >= n, "output buffer too small");
-        float* tmp = nullptr;
-        HIPCHK(hipMalloc(&tmp, n * 4));
+        std::vector<void*> tmp_owned;  // (dalloc / dfree take the capture gate)
+        float* tmp = dalloc<float>((size_t)n, tmp_owned);
         launch_mel_normalize(c->logmel, c->mel_off[clip], nf, c->d.n_mels, c->clip_max, clip, tmp, c->stream);
         hipError_t e = hipMemcpyAsync(out, tmp, n * 4, hipMemcpyDeviceToHost, c->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-        (void)hipFree(tmp);
+        dfree(tmp, tmp_owned);
         HIPCHK(e);
     });
 }
@@ -1971,7 +2029,8 @@ int osw_get_encoder_output(osw_ctx* c, int32_t window, float* out, int64_t out_f
         const int64_t n = (int64_t)T_ENC * c->d.n_audio_state;
         REQUIRE(out_floats >= n, "output buffer too small");
         std::vector<_Float16> tmp(n);
-        HIPCHK(hipMemcpy(tmp.data(), c->E + window * n, n * 2, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpyAsync(tmp.data(), c->E + window * n, n * 2, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
         for (int64_t i = 0; i < n; ++i) out[i] = (float)tmp[i];
     });
 }
@@ -2092,6 +2151,7 @@ int osw_debug_gemm(osw_ctx* c, int32_t M, int32_t N, int32_t K, int32_t variant,
                 "the 8-phase debug variants need N % 8 == 0 (their epilogues store 8-column chunks)");
         std::lock_guard<std::mutex> lk(c->mu);
         DeviceScope dev_scope_((c->device));
+        GateLock gate_(capture_gate());
         std::vector<void*> tmp;
         h16* dA = dalloc<h16>((size_t)M * K, tmp);
         h16* dW = dalloc<h16>((size_t)N * K, tmp);
@@ -2101,8 +2161,8 @@ int osw_debug_gemm(osw_ctx* c, int32_t M, int32_t N, int32_t K, int32_t variant,
         HIPCHK(hipEventCreate(&e0));
         HIPCHK(hipEventCreate(&e1));
         try {
-            HIPCHK(hipMemcpy(dA, A, (size_t)M * K * 2, hipMemcpyHostToDevice));
-            HIPCHK(hipMemcpy(dW, Wt, (size_t)N * K * 2, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpyAsync(dA, A, (size_t)M * K * 2, hipMemcpyHostToDevice, c->stream));
+            HIPCHK(hipMemcpyAsync(dW, Wt, (size_t)N * K * 2, hipMemcpyHostToDevice, c->stream));
             GemmArgs g = gemm_plain(dA, K, dW, nullptr, M, N, K, dC, N, EPI_F32);
             auto run = [&] {
                 if (variant == 3) launch_gemm_skinny(g, dP, c->stream);
@@ -2117,7 +2177,8 @@ int osw_debug_gemm(osw_ctx* c, int32_t M, int32_t N, int32_t K, int32_t variant,
             float t = 0.f;
             HIPCHK(hipEventElapsedTime(&t, e0, e1));
             *ms = t / iters;
-            HIPCHK(hipMemcpy(C, dC, (size_t)M * N * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpyAsync(C, dC, (size_t)M * N * 4, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
         } catch (...) {
             (void)hipEventDestroy(e0);
             (void)hipEventDestroy(e1);
@@ -2127,6 +2188,48 @@ int osw_debug_gemm(osw_ctx* c, int32_t M, int32_t N, int32_t K, int32_t variant,
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
         for (void* p : tmp) (void)hipFree(p);
+    });
+}
+
+int osw_debug_hold_capture(osw_ctx* c, int32_t hold_ms) {
+    return guard([&] {
+        REQUIRE(c, "null ctx");
+        REQUIRE(hold_ms >= 0 && hold_ms <= 10000, "hold_ms out of range");
+        std::lock_guard<std::mutex> lk(c->mu);
+        DeviceScope dev_scope_((c->device));
+        // exactly the locks decode_graph holds around a capture
+        std::unique_lock<std::mutex> no_encoder;
+        if (c->baton) no_encoder = std::unique_lock<std::mutex>(c->baton->mu);
+        GateLock gate_(capture_gate());
+        HIPCHK(hipStreamSynchronize(c->stream));
+        hipGraph_t gr = nullptr;
+        c->capturing = true;
+        try {
+            HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+            HIPCHK(hipMemsetAsync(c->done, 0, sizeof(int), c->stream));  // one captured node
+            const auto t0 = std::chrono::steady_clock::now();
+            while (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(hold_ms)) {
+                std::this_thread::sleep_for(std::chrono::milliseconds(1));
+                hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+                HIPCHK(hipStreamIsCapturing(c->stream, &st));
+                REQUIRE(st == hipStreamCaptureStatusActive, "the capture was invalidated while held");
+            }
+            HIPCHK(hipStreamEndCapture(c->stream, &gr));
+        } catch (...) {
+            c->capturing = false;
+            hipGraph_t junk = nullptr;
+            (void)hipStreamEndCapture(c->stream, &junk);
+            if (junk) (void)hipGraphDestroy(junk);
+            (void)hipGetLastError();
+            throw;
+        }
+        c->capturing = false;
+        REQUIRE(gr != nullptr, "empty capture");
+        hipGraphExec_t ge = nullptr;
+        hipError_t e = hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(gr);
+        HIPCHK(e);
+        (void)hipGraphExecDestroy(ge);
     });
 }
 

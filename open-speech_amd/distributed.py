@@ -13,9 +13,16 @@ stream.  ``run_steps`` then overlaps consecutive steps: while lane 0 decodes ste
 k (HBM- and launch-latency-bound), lane 1 runs step k+1's log-mel and encoder
 (MFMA-bound).  Collectives stay on the calling thread, in step order on every
 rank, so the RCCL call sequence is identical across ranks.
+
+Every torch op here (the scatter / gather collectives, the shard copies) runs on a
+torch stream of its own, which is non-blocking, never on the legacy default stream:
+the lanes capture their decode steps into hipGraphs on first use, and HIP refuses any
+legacy-stream work in the process while a capture is in progress (include/osw.h,
+concurrency contract).
 """
 from __future__ import annotations
 
+import contextlib
 import dataclasses
 from collections import deque
 from concurrent.futures import ThreadPoolExecutor
@@ -38,6 +45,7 @@ class DataParallelTranscriber:
         self.world = dist.get_world_size() if dist else 1
         self.rank = dist.get_rank() if dist else 0
         self.device = device if device is not None else torch.device("cpu")
+        self.stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
         self.B, self.S, self.ctx = clips_per_rank, n_samples, ctx
         assert n_samples % 2 == 0, "int16 PCM travels as int32 pairs"
         self.lanes = [engine] + [engine.sibling() for _ in range(max(1, lanes) - 1)]
@@ -49,8 +57,15 @@ class DataParallelTranscriber:
         self.offsets = np.arange(self.B + 1, dtype=np.int64) * self.S
         self.pool = ThreadPoolExecutor(len(self.lanes)) if len(self.lanes) > 1 else None
 
+    def _on_stream(self):
+        return self.torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
+
     def scatter(self, all_pcm, slot: int = 0) -> None:
         """all_pcm: [world*B, S] int16 tensor on rank 0 (ignored elsewhere)."""
+        with self._on_stream():
+            self._scatter(all_pcm, slot)
+
+    def _scatter(self, all_pcm, slot: int) -> None:
         shard = self.shards[slot]
         if self.world == 1:
             shard.copy_(all_pcm)
@@ -65,13 +80,17 @@ class DataParallelTranscriber:
         return eng.transcribe_batch(list(shard.numpy()), self.cfg)
 
     def _sync(self) -> None:
-        # the scatter/copy ran on torch's current stream; the lanes use their own streams,
+        # the scatter/copy ran on this object's stream; the lanes use their own streams,
         # so wait for this stream only (a device-wide sync would stall on the busy lanes)
-        if self.device.type == "cuda":
-            self.torch.cuda.current_stream(self.device).synchronize()
+        if self.stream is not None:
+            self.stream.synchronize()
 
     def gather(self, outs):
         """Token ids of every clip on rank 0: list of lists in global clip order."""
+        with self._on_stream():
+            return self._gather(outs)
+
+    def _gather(self, outs):
         t = np.full((self.B, self.ctx + 1), -1, np.int32)
         for i, o in enumerate(outs):
             n = min(len(o.tokens), self.ctx)
@@ -155,7 +174,8 @@ class DataParallelTranscriber:
         for i in range(k):  # the scatters in step order (identical on every rank)
             lane, j = i % nl, i // nl
             self.scatter(all_pcm, 0)
-            bufs[lane][j * self.B:(j + 1) * self.B].copy_(self.shards[0])
+            with self._on_stream():
+                bufs[lane][j * self.B:(j + 1) * self.B].copy_(self.shards[0])
             if j == len(steps[lane]) - 1:  # this lane's last shard: start it
                 self._sync()
                 if self.pool is None:

@@ -213,24 +213,29 @@ class _SessionLane(_Worker):
         """('sess', key, reqs) — requests to add to the session (key: the session's, or a
         new one when idle); ('batch', reqs); None when the runner closes."""
         dq, pool = self.dq, self.pool
+        deadline = None     # an idle lane waits for another lane's encoder at most max_pace_ms per call
         with dq.cv:
             while True:
-                if dq.closing or not self.alive:
+                if not self.alive:
                     return None
+                if dq.closing:
+                    # admit nothing more; a lane with windows in flight finishes them first
+                    return None if idle else ("sess", key, [])
                 if dq.items and room > 0:
                     if pool.split and dq.encoding:
                         # another lane's encoder is running: a busy lane keeps decoding, an
-                        # idle one waits for that encoder (bounded) and then takes everything
-                        # that queued meanwhile — the lanes take turns on the encoder
+                        # idle one waits for that encoder (at most max_pace_ms over this
+                        # call) and then takes everything that queued meanwhile — the lanes
+                        # take turns on the encoder
                         if not idle:
                             return ("sess", key, [])
-                        end = time.monotonic() + pool.max_pace_ms / 1000.0
-                        while dq.encoding and not dq.closing and self.alive:
-                            left = end - time.monotonic()
-                            if left <= 0:
-                                break
+                        if deadline is None:
+                            deadline = time.monotonic() + pool.max_pace_ms / 1000.0
+                        left = deadline - time.monotonic()
+                        if left > 0:
                             dq.cv.wait(timeout=left)
-                        continue
+                            continue
+                        # waited max_pace_ms: take requests beside the running encoder
                     if idle:
                         head = dq.items[0]
                         if not session_supported(head.opts):
@@ -381,9 +386,15 @@ class _SessionLane(_Worker):
                 eng.session_end()
             except Exception:  # noqa: BLE001
                 pass
+        # (closing: the loop above drained the flights.)  A lane marked dead because a
+        # sibling lane of its GPU failed hands its unanswered requests to the surviving GPUs
+        # (they restart there: a request's answer is only produced at its end)
         for req, _, _ in flights.values():
             if not req.fut.done():
-                req.fut.set_exception(RuntimeError("runner closed"))
+                if not self.alive:
+                    pool.submit_req(req)
+                else:
+                    req.fut.set_exception(RuntimeError("runner closed"))
 
 
 class BatchRunner:
@@ -424,10 +435,17 @@ class BatchRunner:
 
     @staticmethod
     def is_device_error(e: Exception) -> bool:
-        from ._lib import OswDeviceError
+        """A fault of the GPU itself (its lanes are failed over).  A refused or invalidated
+        stream capture (OSW_ECAPTURE) is not one: the context and the GPU stay usable, so
+        only the requests of that call fail."""
+        from ._lib import OswCaptureError, OswDeviceError
+        if isinstance(e, OswCaptureError):
+            return False
         if isinstance(e, OswDeviceError):
             return True
         s = str(e)
+        if "capture" in s.lower():
+            return False
         return "hipError" in s or "(-100)" in s
 
     def fail_device(self, failed: _Worker) -> bool:
@@ -473,14 +491,19 @@ class BatchRunner:
             with q.cv:
                 q.closing = True
                 q.cv.notify_all()
+        # a lane finishes what it is running (a session lane: its windows in flight, each
+        # request to its end, as the reference's in-flight WhisperModel.transcribe calls
+        # keep their model alive past unload_model)
         for w in self.workers:
-            w.join(timeout=30)
+            w.join(timeout=300)
         for q in self.queues:
             for r in q.items:
                 if not r.fut.done():
                     r.fut.set_exception(RuntimeError("runner closed"))
             q.items.clear()
         for w in self.workers:
+            if w.is_alive():
+                continue   # (a lane still inside a call keeps its context: never destroyed under it)
             close = getattr(w.engine._e, "close", None)
             if close:
                 close()

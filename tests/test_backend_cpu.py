@@ -669,6 +669,128 @@ def test_session_lane_device_error_fails_over():
         runner.close()
 
 
+def test_session_lane_device_error_two_lanes_per_gpu():
+    """GPU 0 has two lanes, both with windows in flight; one fails with a device
+    error.  fail_device marks both dead; the healthy sibling's unanswered requests go to
+    GPU 1 instead of failing with 'runner closed'.  Every request is answered."""
+    from concurrent.futures import Future
+    from open_speech_amd._lib import OswDeviceError
+    from open_speech_amd.runner import BatchRunner, _Req
+    from open_speech_amd.segments import TranscribeOptions
+    from open_speech_amd.tokenizer import WhisperTokenizer
+
+    armed, fired = threading.Event(), []
+    lock = threading.Lock()
+
+    class Eng(FakeEngine):
+        def __init__(self, device, tag, max_batch):
+            super().__init__(D.MICRO_TEST, device, max_batch,
+                             lambda w, i, p, l: WindowOutput([TB, 1000 + tag, TB + 50], -1.0, 0.01, ST.first_lang))
+            self.device, self.step_sleep = device, 0.02
+            self.began = threading.Event()
+
+        def session_step(self, max_chunks=1, refill_min=1):
+            if max_chunks:
+                self.began.set()
+            with lock:
+                fire = self.device == 0 and armed.is_set() and not fired
+                if fire:
+                    fired.append(self)
+            if fire:
+                raise OswDeviceError("osw_session_step failed (-100): hipErrorLaunchFailure", -100)
+            return super().session_step(max_chunks, refill_min)
+
+    l0, l1, b = Eng(0, 1, 2), Eng(0, 1, 2), Eng(1, 3, 8)
+    runner = BatchRunner([l0, l1, b], WhisperTokenizer(51866), continuous=True, split=False)
+    try:
+        opts = TranscribeOptions(language="en")
+        # long clips (many windows each): two requests per lane of GPU 0 (max_batch 2)
+        reqs = [_Req(synth.chirp_clip(i, 120.0), opts, Future()) for i in range(4)]
+        with runner.queues[0].cv:
+            for r in reqs:
+                r.t_enq = time.monotonic()
+                runner.queues[0].items.append(r)
+            runner.queues[0].cv.notify_all()
+        assert l0.began.wait(10) and l1.began.wait(10)
+        assert all(not r.fut.done() for r in reqs)
+        armed.set()
+        for r in reqs:
+            res = r.fut.result(timeout=60)
+            assert res.segments and all(sg.tokens in ([TB, 1001, TB + 50], [TB, 1003, TB + 50]) for sg in res.segments)
+        assert fired and not runner.workers[0].alive and not runner.workers[1].alive and runner.workers[2].alive
+        # the sibling that did not fail had requests in flight: they finished on GPU 1
+        sib = l1 if fired[0] is l0 else l0
+        assert sib.calls and b.calls
+        assert sum(any(sg.tokens == [TB, 1003, TB + 50] for sg in r.fut.result().segments) for r in reqs) >= 3
+    finally:
+        runner.close()
+
+
+def test_capture_error_is_not_a_device_fault():
+    """an OSW_ECAPTURE error (a refused / invalidated stream capture) fails the
+    requests of that call only; the GPU is not marked dead and keeps serving."""
+    from concurrent.futures import Future
+    from open_speech_amd._lib import OswCaptureError
+    from open_speech_amd.runner import BatchRunner, _Req
+    from open_speech_amd.segments import TranscribeOptions
+    from open_speech_amd.tokenizer import WhisperTokenizer
+
+    assert not BatchRunner.is_device_error(OswCaptureError("osw_decode_windows failed (-102): x", -102))
+    assert not BatchRunner.is_device_error(RuntimeError(
+        "osw_decode_windows failed (-100): hipGetLastError(): operation failed due to a previous error during capture"))
+
+    class Eng(FakeEngine):
+        def __init__(self, device):
+            super().__init__(D.MICRO_TEST, device, 4)
+            self.device, self.n = device, 0
+
+        def session_step(self, max_chunks=1, refill_min=1):
+            self.n += 1
+            if self.n == 2:
+                raise OswCaptureError("osw_session_step failed (-102): operation would make the legacy stream "
+                                      "depend on a capturing blocking stream", -102)
+            return super().session_step(max_chunks, refill_min)
+
+    a, b = Eng(0), Eng(1)
+    runner = BatchRunner([a, b], WhisperTokenizer(51866), continuous=True)
+    try:
+        r1 = _Req(synth.chirp_clip(1, 3.0), TranscribeOptions(language="en"), Future())
+        runner.workers[0].q.put(r1)
+        with pytest.raises(OswCaptureError):
+            r1.fut.result(timeout=10)
+        assert runner.workers[0].alive and runner.queues[0].alive
+        r2 = _Req(synth.chirp_clip(2, 3.0), TranscribeOptions(language="en"), Future())
+        runner.workers[0].q.put(r2)
+        assert r2.fut.result(timeout=10).segments
+        assert not b.calls    # nothing moved to the other GPU
+    finally:
+        runner.close()
+
+
+def test_session_lane_close_drains_flights():
+    """closing the runner (unload_model) lets a session lane finish the requests
+    it is decoding instead of failing them with 'runner closed'."""
+    from concurrent.futures import Future
+    from open_speech_amd.runner import BatchRunner, _Req
+    from open_speech_amd.segments import TranscribeOptions
+    from open_speech_amd.tokenizer import WhisperTokenizer
+
+    e = FakeEngine(D.MICRO_TEST, 0, 4)
+    e.step_sleep = 0.01
+    runner = BatchRunner([e], WhisperTokenizer(51866), continuous=True)
+    reqs = [_Req(synth.chirp_clip(i, 60.0), TranscribeOptions(language="en"), Future()) for i in range(2)]
+    for r in reqs:
+        runner.submit_req(r)
+    deadline = time.monotonic() + 10
+    while not e.batches and time.monotonic() < deadline:
+        time.sleep(0.005)
+    assert e.batches, "the lane never started decoding"
+    runner.close()
+    for r in reqs:
+        assert r.fut.result(timeout=1).segments
+    assert e.closed
+
+
 def test_session_lane_error_before_flight_fails_taken_requests():
     """An error while opening the session (before the taken requests are in flight) fails
     those requests instead of dropping them (a request is never left unanswered)."""

@@ -38,7 +38,17 @@ from open_speech_amd.tokenizer import WhisperTokenizer, get_suppressed_tokens  #
 
 HBM_PEAK_GBS = 8000.0        # MI355X spec (MI355X_MICROARCH.md)
 MFMA_F16_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA spec
+VALU_F32_PEAK_TFLOPS = 157.3   # fp32 vector spec (MI355X_MICROARCH.md)
+# VALU flops of mel_logmel_kernel per frame (csrc/mel.hip): stage 1, 25 real 16-point DFTs
+# (16 window mults, 9 bins x 16 x 2 FMA, 16 complex twiddles) = 25 x 688; stage 2, 201 bins x
+# 25 complex MACs x 8 + 201 x 3 (power); stage 3, the slaney bank's 394 taps (128 mels) x 2 +
+# 128 log10 + 128 max
+MEL_FLOPS_PER_FRAME = 25 * 688 + 201 * 25 * 8 + 201 * 3 + 394 * 2 + 2 * 128
 
+
+# length control of the serving benches (HipWhisperBackend(length_control=...)): random
+# weights never emit <|endoftext|>, so each window ends after 4 tokens per second of audio
+LENGTH_CONTROL_TPS = 4.0
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
@@ -192,14 +202,13 @@ def rest_mixed(callers: int, calls: int, model: str = "random:large-v3-turbo") -
     from open_speech_amd.audio import pcm_to_wav
     from open_speech_amd.backend import HipWhisperBackend
 
-    os.environ.setdefault("STT_HIP_TOKENS_PER_SEC", "4")
     lens = (4.0, 12.0, 30.0, 45.0, 75.0, 20.0, 8.0, 60.0)
     wavs = [pcm_to_wav(synth.chirp_clip(800 + i, x).tobytes(), 16000) for i, x in enumerate(lens)]
     out = {"callers": callers, "calls_per_caller": calls, "clip_s": list(lens), "think_ms_mean": 40}
     prev = os.environ.get("STT_HIP_CONTINUOUS")
     for mode, flag in (("continuous", "1"), ("batch_at_a_time", "0")):
         os.environ["STT_HIP_CONTINUOUS"] = flag
-        be = HipWhisperBackend()
+        be = HipWhisperBackend(length_control=LENGTH_CONTROL_TPS)
         be.load_model(model)
         be.transcribe(audio=wavs[0], model=model, language=None, response_format="json")   # warm
         lat, lock = [], threading.Lock()
@@ -243,17 +252,16 @@ def stream_sessions(n_sessions: int, speech_s: float, model: str = "random:large
     silence finalises (_finalize_utterance :422-481).  Calls go through a 4-thread
     executor like _streaming_executor (:50-52), so at most 4 are in flight and the
     backend batches them across sessions.  Random weights never emit <|endoftext|>: the
-    backend cuts each window at 4 tokens per second of audio (STT_HIP_TOKENS_PER_SEC,
-    bench-only).  The reference's default beam_size 5 is used."""
+    backend cuts each window at 4 tokens per second of audio (its bench-only
+    ``length_control``; a backend passed in must have been built with it).  The reference's default beam_size 5 is used."""
     import asyncio
     from concurrent.futures import ThreadPoolExecutor
 
     from open_speech_amd.audio import pcm_to_wav
     from open_speech_amd.backend import HipWhisperBackend
 
-    os.environ.setdefault("STT_HIP_TOKENS_PER_SEC", "4")
     own = backend is None
-    be = HipWhisperBackend() if own else backend
+    be = HipWhisperBackend(length_control=LENGTH_CONTROL_TPS) if own else backend
     be.load_model(model)
     ex = ThreadPoolExecutor(max_workers=4, thread_name_prefix="stream-transcribe")
     chunk = 1600
@@ -546,6 +554,18 @@ def main(argv=None):
 
         live = [k for k in cands if cands[k][2] > 0]
         roofs = {k: roofline(k) for k in live}
+        if "log_mel" in roofs:
+            # the log-mel kernel's arithmetic against the VALU fp32 peak (its bytes are ~1 % of
+            # HBM time): MEL_FLOPS_PER_FRAME x 3001 frames per 30 s clip
+            ms, _, nl, _ = cands["log_mel"]
+            fl = MEL_FLOPS_PER_FRAME * 3001 * B * nl
+            ach = fl / (ms * 1e-3) / 1e12
+            roofs["log_mel"]["valu"] = {
+                "bound": "valu", "achieved": round(ach, 2), "peak": VALU_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / VALU_F32_PEAK_TFLOPS, 4), "flop_per_frame": MEL_FLOPS_PER_FRAME,
+                "frac_of_unpacked": round(ach / (VALU_F32_PEAK_TFLOPS / 2), 4),
+                "note": "spec vector peak counts packed fp32 (v_pk_fma_f32); this library is built without "
+                        "packed fp32 (csrc/Makefile NOPK), whose ceiling is half of it"}
         roof = dict(roofs[max(live, key=lambda k: cands[k][0])])
         roof["measured"] = "isolated roofline pass after the timed region (1 lane, HIP events on the lane's stream)"
         stages = {k: {"ms": round(v[0], 2), "launches": int(v[2])} for k, v in cands.items()}

@@ -80,7 +80,11 @@ class HipWhisperBackend:
 
     name = "faster-whisper"
 
-    def __init__(self, engine_factory=None) -> None:
+    def __init__(self, engine_factory=None, length_control: float | None = None) -> None:
+        """``length_control`` (benchmarks only, not a reference option): end every window
+        after this many tokens per second of audio, since random weights never emit
+        <|endoftext|> (segments.TranscribeOptions.tokens_per_second)."""
+        self._length_control = length_control
         self._models: dict[str, Any] = {}
         self._loaded_at: dict[str, float] = {}
         self._last_used: dict[str, float] = {}
@@ -256,12 +260,11 @@ class HipWhisperBackend:
                        prompt: str | None = None) -> dict[str, Any]:
         m = self._ensure_model(model_id)
         pcm = decode_audio_bytes(audio)
-        tps = os.environ.get("STT_HIP_TOKENS_PER_SEC")  # bench-only length control (segments.py)
         opts = TranscribeOptions(task=task, language=language if (language and task == "transcribe") else None,
                                  initial_prompt=prompt or None, temperature=float(temperature or 0.0),
                                  beam_size=int(os.environ.get("STT_HIP_BEAM_SIZE", "5")),
                                  best_of=int(os.environ.get("STT_HIP_BEST_OF", "5")),
-                                 tokens_per_second=float(tps) if tps else None)
+                                 tokens_per_second=self._length_control)
         res = m.runner.transcribe(pcm, opts)
         return shape_response(task, res, response_format)
 

@@ -167,6 +167,7 @@ int tiled_ksplit(int M, int N, int K);
 void launch_gemm_tiled_partial(const GemmArgs& g, float* part, int ks, hipStream_t s);
 int launch_gemm_skinny_partial(const GemmArgs& g, float* part, hipStream_t s);
 struct ProArgs;
+int launch_gemm_skinny_gelu_tail(const GemmArgs& g, float* part, const ProArgs& pa, hipStream_t s);
 int launch_gemm_skinny_pro(const GemmArgs& g, int pro, const ProArgs& pa, bool direct, float* part, hipStream_t s,
                            bool select = false);
 void launch_layernorm(const float* x, int64_t M, int D, const float* g, const float* b, h16* y, hipStream_t s);

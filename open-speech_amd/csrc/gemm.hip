@@ -1259,7 +1259,7 @@ __device__ __forceinline__ void fused_select_row(float x, int col, bool valid, c
     __hip_atomic_store(F.pos, step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int MT, bool DIRECT, int EPI, bool LO, int PRO = PRO_NONE, bool SEL = false>
+template <int MT, bool DIRECT, int EPI, bool LO, int PRO = PRO_NONE, bool SEL = false, int TAIL = TAIL_NONE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL ? 4 : 1, 8))) void gemm_skinny_kernel(GemmArgs g, int kc, float* __restrict__ part, ProArgs pa) {
     // Workgroup = 64 columns x one kc-deep K range; wave = 16 columns.  The
     // activation rows (M <= 64) of each CKK-deep K chunk are staged ONCE per
@@ -1516,21 +1516,69 @@ store:
         fused_select_row(acc[0][0], col, valid, pa.sel, sel_pre);
         return;
     }
-    if (col >= g.N) return;
+    if (col < g.N) {
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+        for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int m = mb + mt * 16 + gq * 4 + i;
-            if (m >= g.M) continue;
-            if constexpr (DIRECT) store_one<EPI>(g, m, col, acc[mt][i]);
-            // slabs are written through L2 (device-scope stores): no dirty lines left for
-            // the kernel-boundary write-back to drain before the consumer can start.  (Staging
-            // the tile through LDS for 8-B coalesced stores, as gemm_wide_kernel does, cost
-            // more in barriers than it saved: 7.7 -> 8.3 us at 64 rows, measured.)
-            else __hip_atomic_store(&part[((int64_t)ks * g.M + m) * g.N + col], acc[mt][i], __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT);
+            for (int i = 0; i < 4; ++i) {
+                const int m = mb + mt * 16 + gq * 4 + i;
+                if (m >= g.M) continue;
+                if constexpr (DIRECT) store_one<EPI>(g, m, col, acc[mt][i]);
+                // slabs are written through L2 (device-scope stores): no dirty lines left for
+                // the kernel-boundary write-back to drain before the consumer can start.  (Staging
+                // the tile through LDS for 8-B coalesced stores, as gemm_wide_kernel does, cost
+                // more in barriers than it saved: 7.7 -> 8.3 us at 64 rows, measured.)
+                else __hip_atomic_store(&part[((int64_t)ks * g.M + m) * g.N + col], acc[mt][i], __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+            }
+    }
+    if constexpr (TAIL == TAIL_GELU) {
+        static_assert(!DIRECT && PRO == PRO_NONE && !SEL, "the GELU tail reduces split-K slabs");
+        // the last of the block's ks workgroups reduces its 64 columns x ROWS rows; every
+        // slab store of this workgroup is complete at device scope before its ticket
+        __shared__ int t_last;
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        const int nz = (g.M + ROWS - 1) / ROWS, nks = g.K / kc;
+        if (threadIdx.x == 0) {
+            int* tk = pa.tail_ticket + bx * nz + bz;
+            t_last = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nks - 1;
+            if (t_last) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        __syncthreads();
+        if (!t_last) return;
+        // element e = r * 64 + c of the block, EPT per thread; the slabs were written by other
+        // workgroups of this launch (other XCDs): device-scope loads.  Every element's loads of
+        // a batch of 8 slabs are issued before any is added; the adds in gelu_reduce_one's order
+        constexpr int EPT = ROWS * 64 / 256;
+        const int64_t slab = (int64_t)g.M * g.N;
+        int64_t off[EPT];
+        float v[EPT];
+        bool ok[EPT];
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) {
+            const int e = threadIdx.x + 256 * j, m = mb + (e >> 6), n = bx * 64 + (e & 63);
+            ok[j] = m < g.M && n < g.N;
+            off[j] = (int64_t)min(m, g.M - 1) * g.N + min(n, g.N - 1);
+            v[j] = pa.bias[min(n, g.N - 1)];
+        }
+        for (int k0 = 0; k0 < nks; k0 += 8) {
+            float p[EPT][8];
+#pragma unroll
+            for (int j = 0; j < EPT; ++j)
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    p[j][q] = __hip_atomic_load(part + (int64_t)min(k0 + q, nks - 1) * slab + off[j], __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int j = 0; j < EPT; ++j)
+#pragma unroll
+                for (int q = 0; q < 8; ++q) v[j] += k0 + q < nks ? p[j][q] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < EPT; ++j)
+            if (ok[j]) split_h16(gelu_erf(v[j]), pa.tail_y, pa.tail_y + pa.tail_lo, off[j]);
+    }
 }
 
 // Wide-N GEMM for the decoder (logits: 64-row tiles x the 51866 vocabulary columns;
@@ -1771,6 +1819,11 @@ int skinny_ksplit(int N, int K) {
     const int nbn = (N + 63) / 64;
     if (nbn >= 512) return 1;
     if (K % 256) return K / 128;
+    // OSW_SKINNY_KC=k (A/B switch): K per workgroup at least k (fewer slabs, fewer workgroups)
+    static const int kc_min = getenv("OSW_SKINNY_KC") ? atoi(getenv("OSW_SKINNY_KC")) : 256;
+    if (kc_min > 256)
+        for (int c = kc_min; c <= K; c += 128)
+            if (K % c == 0 && c % 128 == 0) return K / c;
     int kc = 256;
     while ((K / kc) * nbn > 2048 && K % (2 * kc) == 0) kc *= 2;
     return K / kc;
@@ -1807,6 +1860,29 @@ int launch_gemm_skinny_partial(const GemmArgs& g0, float* part, hipStream_t s) {
         default: OSW_SKINNY_PART(4); break;
     }
 #undef OSW_SKINNY_PART
+    return ks;
+}
+
+// launch_gemm_skinny_partial + the GELU tail (ProArgs::tail_*): fc1 of 9..64 decoder rows,
+// whose reduce + bias + GELU then needs no kernel of its own.  Returns ksplit.
+int launch_gemm_skinny_gelu_tail(const GemmArgs& g0, float* part, const ProArgs& pa, hipStream_t s) {
+    static const bool no_pair = getenv("OSW_SKINNY_NOPAIR") != nullptr;
+    GemmArgs g = g0;
+    g.preload_w = 1;
+    const int ks = skinny_ksplit(g.N, g.K);
+    const int gr = (g.A_lo && g.M > 32) ? 32 : 64;
+    const int nz = (g.M + gr - 1) / gr;
+    g.pair_rows = (nz > 1 && !no_pair) ? 1 : 0;
+    const int units = (g.N + 63) / 64 * ks;
+    const dim3 grid = g.pair_rows ? dim3((unsigned)(8 * ((units + 7) / 8) * nz), 1, 1)
+                                  : dim3((g.N + 63) / 64, ks, nz);
+    const int kc = g.K / ks;
+    if (!g.A_lo || g.M > 64 || g.N % 64)
+        throw std::invalid_argument("GELU tail: hi/lo operand, <= 64 rows, N a multiple of 64");
+    switch (std::min(g.M, gr) <= 16 ? 1 : 2) {
+        case 1: gemm_skinny_kernel<1, false, EPI_F32, true, PRO_NONE, false, TAIL_GELU><<<grid, 256, 0, s>>>(g, kc, part, pa); break;
+        default: gemm_skinny_kernel<2, false, EPI_F32, true, PRO_NONE, false, TAIL_GELU><<<grid, 256, 0, s>>>(g, kc, part, pa); break;
+    }
     return ks;
 }
 

@@ -280,6 +280,7 @@ struct osw_ctx {
     float* part2 = nullptr;    // second slab buffer of the fused small-batch step (<= PRO_ROWS rows)
     float* xws = nullptr;      // cross-attention per-chunk partials [R][H][XCHUNKS][XPART]
     int* xticket = nullptr;    // cross-attention arrival tickets [B][H] (zero between launches)
+    int* tail_ticket = nullptr; // split-K GEMM tails (ProArgs::tail_ticket)
     int* sel_arrive = nullptr; // select arrival counters: rows finalised + per-row slice tickets (zero between launches)
     int* budget = nullptr;     // per-row token budgets (osw_decode_opts::token_budget)
     unsigned long long* seed_d = nullptr;  // sampling seed of the current decode call
@@ -613,6 +614,8 @@ void setup_workspace(osw_ctx* c) {
     HIPCHK(hipMemsetAsync(c->xticket, 0, (size_t)B * d.n_text_head * sizeof(int), c->stream));
     c->budget = dalloc<int>(R, o);
     c->seed_d = dalloc<unsigned long long>(1, o);
+    c->tail_ticket = dalloc<int>(4096, o);  // GEMM tails: [column blocks x row groups] (zero between launches)
+    HIPCHK(hipMemsetAsync(c->tail_ticket, 0, 4096 * sizeof(int), c->stream));
     c->sel_arrive = dalloc<int>(1 + R, o);  // [0] rows finalised, [1 + row] slice tickets
     HIPCHK(hipMemsetAsync(c->sel_arrive, 0, (1 + (size_t)R) * sizeof(int), c->stream));
     {
@@ -929,6 +932,12 @@ bool decoder_step(osw_ctx* c, int nb, int group, bool gather, const SelFuse* sf 
     }
     static const bool no_gelu_pro = getenv("OSW_NO_GELU_PRO") != nullptr;  // A/B switch
     const bool gelu_pro = nb <= GELU_ROWS && !no_gelu_pro && 4 * D / skinny_ksplit(D, 4 * D) <= GELU_KC;
+    // OSW_GELU_TAIL=1: fc1's last workgroup per column block reduces + GELUs its slabs (no
+    // reduce kernel).  Measured slower in the 3-lane headline (5018 / 5016 vs 5049 audio-s/s,
+    // profiles/r06_b_gelu_tail_ab.txt): with the lanes overlapping, a launch fewer buys less
+    // than the serial tail costs, so it is opt-in
+    static const bool gelu_tail_on = getenv("OSW_GELU_TAIL") && getenv("OSW_GELU_TAIL")[0] == '1';
+    const bool gelu_tail = !gelu_pro && nb <= 64 && gelu_tail_on && (4 * D) % 64 == 0;
     // x = tok_emb[tok] + pos_emb[pos]; xdn = LN1_0(x)
     launch_dec_resid_ln(nullptr, 0, nb, D, nullptr, c->xd, WF(c, "dec.l0.ln1.g"), WF(c, "dec.l0.ln1.b"), c->xdn, lo_d,
                         WH(c, "dec.tok"), WF(c, "dec.pos"), c->cur_tok, c->pos, ctx, d.n_vocab, c->stream, c->row_pos);
@@ -952,8 +961,23 @@ bool decoder_step(osw_ctx* c, int nb, int group, bool gather, const SelFuse* sf 
                             c->xdn, lo_d, nullptr, nullptr, nullptr, nullptr, ctx, d.n_vocab, c->stream);
         // (a whole-K fc1 with the GELU epilogue fused has only N/64 = 80 workgroups at
         // turbo: 22.7 us vs 9.6 + 4.7 us for split-K + reduce, measured)
-        ks = partial(c->xdn, D, p + ".fc1.w", 4 * D, D);
         const float* fc2_part = c->part;
+        if (gelu_tail) {
+            // 9..64 rows: split-K fc1 whose last workgroup per column block reduces that
+            // block's slabs + bias + GELU (TAIL_GELU): no reduce kernel
+            GemmArgs g = gemm_plain(c->xdn, D, WH(c, p + ".fc1.w"), nullptr, nb, 4 * D, D, nullptr, 0, EPI_F32);
+            g.Wf = WFR(c, p + ".fc1.w");
+            g.A_lo = c->xdn + lo_d;
+            ProArgs pt{};
+            pt.bias = WF(c, p + ".fc1.b");
+            pt.tail_ticket = c->tail_ticket;
+            pt.tail_y = c->dh;
+            pt.tail_lo = lo_4d;
+            launch_gemm_skinny_gelu_tail(g, c->part, pt, c->stream);
+            HIPCHK(hipGetLastError());
+            ks = partial(c->dh, 4 * D, p + ".fc2.w", D, 4 * D);
+        } else {
+        ks = partial(c->xdn, D, p + ".fc1.w", 4 * D, D);
         if (gelu_pro) {
             // <= 8 rows: the GELU reduce is fc2's prologue (each workgroup reduces only its own
             // K range of the fc1 slabs, resln.h), fc2's slabs go to part2
@@ -966,6 +990,7 @@ bool decoder_step(osw_ctx* c, int nb, int group, bool gather, const SelFuse* sf 
         } else {
             launch_dec_reduce_gelu(c->part, ks, nb, 4 * D, WF(c, p + ".fc1.b"), c->dh, lo_4d, c->stream);
             ks = partial(c->dh, 4 * D, p + ".fc2.w", D, 4 * D);
+        }
         }
         const std::string nx = l + 1 < L ? "dec.l" + std::to_string(l + 1) + ".ln1" : std::string("dec.lnpost");
         launch_dec_resid_ln(fc2_part, ks, nb, D, WF(c, p + ".fc2.b"), c->xd, WF(c, nx + ".g"), WF(c, nx + ".b"), c->xdn,

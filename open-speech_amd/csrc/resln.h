@@ -192,7 +192,15 @@ struct ProArgs {
     int ks;
     const float* bias;
     SelFuse sel;         // the batch-1 logits GEMM with the selection in its epilogue (decode.h)
+    // TAIL_GELU (split-K partial mode): the last of the ks workgroups of a (64-column block,
+    // row group) to finish reduces the block's slabs: y = gelu(bias + Σ_k part[k]) as a
+    // hi/lo pair at tail_y[m * N + n] / tail_y[tail_lo + m * N + n], exactly as
+    // dec_reduce_gelu_kernel (gelu_reduce_one's order), so that kernel is not launched.
+    int* tail_ticket;    // [column blocks x row groups], zero between launches
+    h16* tail_y;
+    int64_t tail_lo;
 };
+enum Tail : int { TAIL_NONE = 0, TAIL_GELU = 1 };
 
 // fc1 -> fc2 operand: fp16 pair of gelu(bias + Σ_k part[k][r][n]), k in order (the order of
 // dec_reduce_gelu_kernel, which shares this function)

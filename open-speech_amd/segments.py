@@ -55,7 +55,7 @@ class TranscribeOptions:
     # faster-whisper's max_new_tokens: a window's decode stops after this many sampled
     # tokens (max_length = prompt length + max_new_tokens, which may not exceed 448)
     max_new_tokens: int | None = None
-    # bench-only length control (STT_HIP_TOKENS_PER_SEC): random weights never emit
+    # bench-only length control (HipWhisperBackend(length_control=...)): random weights never emit
     # <|endoftext|>, so each window's decode is cut at ceil(rate * window seconds) + 2
     tokens_per_second: float | None = None
 

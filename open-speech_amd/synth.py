@@ -43,6 +43,12 @@ def tone_clip(seconds: float = 7.3, freq: float = 440.0) -> np.ndarray:
     return _to_int16_at_dbfs(np.sin(2 * np.pi * freq * t), -18.0)
 
 
+def noise_clip(i: int, seconds: float = 30.0) -> np.ndarray:
+    """White noise at -18 dBFS, seeded by ``numpy.random.default_rng(i)``."""
+    x = np.random.default_rng(i).standard_normal(int(round(seconds * SR)))
+    return _to_int16_at_dbfs(x, -18.0)
+
+
 def silence_clip(seconds: float = 5.0) -> np.ndarray:
     return np.zeros(int(round(seconds * SR)), dtype=np.int16)
 

@@ -189,7 +189,7 @@ def test_backend_default_config_matches_oracle_seek_loop(monkeypatch, tmp_path):
     from open_speech_amd.tokenizer import WhisperTokenizer, get_suppressed_tokens
 
     for k in ("STT_HIP_BEAM_SIZE", "STT_HIP_LANES", "STT_HIP_MAX_BATCH", "STT_HIP_BATCH_GAP_MS",
-              "STT_HIP_BATCH_WAIT_MS", "STT_HIP_TOKENS_PER_SEC"):
+              "STT_HIP_BATCH_WAIT_MS"):
         monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("STT_HIP_GPUS", "0")
     monkeypatch.setenv("STT_HIP_CONTINUOUS", "0")  # batch at a time (the continuous form: below)
@@ -300,7 +300,7 @@ def test_backend_continuous_matches_oracle_seek_loop(monkeypatch, tmp_path):
     from open_speech_amd.tokenizer import WhisperTokenizer, get_suppressed_tokens
 
     for k in ("STT_HIP_BEAM_SIZE", "STT_HIP_LANES", "STT_HIP_MAX_BATCH", "STT_HIP_BATCH_GAP_MS",
-              "STT_HIP_BATCH_WAIT_MS", "STT_HIP_TOKENS_PER_SEC", "STT_HIP_SPREAD_MS", "STT_HIP_REFILL_MIN"):
+              "STT_HIP_BATCH_WAIT_MS", "STT_HIP_SPREAD_MS", "STT_HIP_REFILL_MIN"):
         monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("STT_HIP_GPUS", "0")
     monkeypatch.setenv("STT_HIP_CONTINUOUS", "1")

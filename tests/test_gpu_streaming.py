@@ -24,13 +24,12 @@ def test_streaming_sessions_equal_cold_single_calls(monkeypatch, sessions, speec
     """(8, 2 s, max batch 8): a quick form.  (32, 6 s, backend defaults): BASELINE
     configs[4] at its stated size, ~2000 calls, every one re-checked cold."""
     import bench
-    monkeypatch.setenv("STT_HIP_TOKENS_PER_SEC", "4")    # random weights never emit <|endoftext|>
     if max_batch:
         monkeypatch.setenv("STT_HIP_MAX_BATCH", max_batch)
     else:
         monkeypatch.delenv("STT_HIP_MAX_BATCH", raising=False)
     monkeypatch.setenv("STT_HIP_GPUS", "0")
-    be = HipWhisperBackend()
+    be = HipWhisperBackend(length_control=bench.LENGTH_CONTROL_TPS)  # random weights never emit <|endoftext|>
     try:
         rec = []
         stats = bench.stream_sessions(sessions, speech_s, model=MID, backend=be, record=rec)

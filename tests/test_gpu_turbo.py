@@ -160,11 +160,14 @@ def test_turbo_beam5_batch64_equals_single_windows(turbo):
 
 
 # --------------------------------------------------------------------------- text goldens
-# tests/golden/turbo_text.npz (tools/make_golden.py gen_turbo_text): the same model with the
-# "text" positional table (weights.text_positional), so greedy decoding emits varied text:
-# ~440 distinct ids in 445 steps per clip, golden top-2 margin >= 0.04 at every step (meta.json
-# "turbo_text"), three clips.  Free-running ids must be identical over all 445 steps; a
-# decoder that copies its previous token, or drops a layer, cannot pass.
+# tests/golden/turbo_text.npz (tools/make_golden.py gen_turbo_text): the same model with a
+# constructed positional table (construct_audio_table, stored as pos_table): each position
+# leans to a pseudo-random text token, and at most positions to a second token as well, with
+# the clip's audio (through the cross-attention) deciding between them.  Three spectrally
+# distinct clips (chirp, 440 Hz tone, white noise); every pair differs at >= 100 of the 445
+# ids; the golden top-2 margins are in meta.json "turbo_text".  Free-running ids must be
+# identical over all 445 steps; a decoder that copies its previous token, drops a layer or
+# ignores the encoder cannot pass.
 TEXT = os.path.join(GOLD, "turbo_text.npz")
 
 
@@ -177,16 +180,34 @@ def _meta(key):
 def turbo_text():
     d = D.LARGE_V3_TURBO
     m = _meta("turbo_text")
+    z = np.load(TEXT)
     eng = WhisperEngine(d, device=0, max_batch=8)
     eng.init_random(seed=m["seed"], text_pos=m["text_pos"])
+    # the constructed, audio-dependent positional table (tools/make_golden.py construct_audio_table)
+    eng.set_weight("dec.pos", z["pos_table"])
     sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
-    yield d, eng, sup, np.load(TEXT), m
+    yield d, eng, sup, z, m
     eng.close()
+
+
+TEXT_CLIPS = ["chirp0", "tone", "noise"]
 
 
 def _text_clip(name):
     return {"chirp0": lambda: synth.chirp_clip(0, 30.0), "tone": lambda: synth.tone_clip(30.0),
-            "chirp1": lambda: synth.chirp_clip(1, 30.0)}[name]()
+            "noise": lambda: synth.noise_clip(5, 30.0)}[name]()
+
+
+def test_turbo_text_golden_depends_on_audio(turbo_text):
+    """the golden ids are a function of the audio — every pair of the
+    three clips differs at >= 100 of the 445 positions (a decoder whose cross-attention
+    ignored the encoder would emit one sequence for all three)."""
+    d, eng, sup, z, m = turbo_text
+    for i, a in enumerate(TEXT_CLIPS):
+        for b in TEXT_CLIPS[i + 1:]:
+            x, y = z[a + "/ids"], z[b + "/ids"]
+            assert len(x) == len(y) == 445
+            assert int((x != y).sum()) >= 100, (a, b)
 
 
 def _lsm_err(out_logits, z, pre, n_steps):
@@ -204,7 +225,7 @@ def _lsm_err(out_logits, z, pre, n_steps):
     return max(errs), n_full
 
 
-@pytest.mark.parametrize("clip", ["chirp0", "tone", "chirp1"])
+@pytest.mark.parametrize("clip", TEXT_CLIPS)
 def test_turbo_text_greedy_ids_exact(turbo_text, clip):
     """Varied-text golden, one window: every one of the 445 greedy ids identical, language
     and no-speech prob equal, and the log-softmax of the raw logits within 1e-3 (over the
@@ -217,7 +238,8 @@ def test_turbo_text_greedy_ids_exact(turbo_text, clip):
     enc = eng.encoder_output(0)
     np.testing.assert_allclose(np.linalg.norm(enc.astype(np.float64), axis=1), z[pre + "enc_rownorm"], rtol=1e-3)
     want = z[pre + "ids"].tolist()
-    assert len(set(want)) >= 150 and len(want) >= 300   # the golden itself is discriminative
+    assert len(set(want)) >= 150 and len(want) >= 300   # the golden itself is discriminative (and see
+                                                        # test_turbo_text_golden_depends_on_audio)
     out = eng.decode(1, DecodeConfig(suppress_tokens=sup), dump_steps=len(want) + 1)[0]
     assert out.language == int(z[pre + "language"])
     assert abs(out.no_speech_prob - float(z[pre + "no_speech_prob"])) < 1e-3
@@ -236,7 +258,7 @@ def test_turbo_text_greedy_ids_exact(turbo_text, clip):
 def test_turbo_text_batch_equals_golden(turbo_text):
     """The three clips in one batch (3 decoder rows): every window's ids equal the golden."""
     d, eng, sup, z, m = turbo_text
-    names = ["chirp0", "tone", "chirp1"]
+    names = TEXT_CLIPS
     outs = eng.transcribe_batch([_text_clip(n) for n in names], DecodeConfig(suppress_tokens=sup))
     for n, o in zip(names, outs):
         assert o.tokens == z[n + "/ids"].tolist(), n

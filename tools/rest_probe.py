@@ -25,8 +25,7 @@ C = int(sys.argv[1]) if len(sys.argv) > 1 else 16
 R = int(sys.argv[2]) if len(sys.argv) > 2 else 6
 J = float(sys.argv[3]) if len(sys.argv) > 3 else 40.0
 MID = "random:large-v3-turbo"
-os.environ.setdefault("STT_HIP_TOKENS_PER_SEC", "4")
-be = HipWhisperBackend()
+be = HipWhisperBackend(length_control=4.0)
 be.load_model(MID)
 MIX = len(sys.argv) > 4 and sys.argv[4] == "mix"
 LENS = (4.0, 12.0, 30.0, 45.0, 75.0, 20.0, 8.0, 60.0) if MIX else (30.0,) * 8

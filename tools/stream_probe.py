@@ -21,8 +21,7 @@ from open_speech_amd.backend import HipWhisperBackend  # noqa: E402
 R = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 SEQ_ONLY = "--sequential-only" in sys.argv
 MID = "random:large-v3-turbo"
-os.environ.setdefault("STT_HIP_TOKENS_PER_SEC", "4")
-be = HipWhisperBackend()
+be = HipWhisperBackend(length_control=4.0)
 be.load_model(MID)
 if os.environ.get("STREAM_PROBE_MAPS"):   # shared-object map, to attribute a native crash's frames
     with open("/proc/self/maps") as src, open(os.environ["STREAM_PROBE_MAPS"], "w") as dst:

@@ -237,6 +237,12 @@ typedef struct osw_session_window {
     int32_t token_budget;     /* length control (benches): <= 0 none */
     int32_t n_prefix;         /* previous-text prompt tokens before <|startoftranscript|> */
     const int32_t* prefix;    /* <|startofprev|> and the previous tokens, or NULL */
+    /* >= 0: the caller's key of the window's clip.  The first window of a key brings the
+     * clip's PCM; its log-mel is computed once and stays on the device, so later windows of
+     * the same key pass no samples (offsets[i] == offsets[i+1]) and are staged from it,
+     * until osw_session_release_clip(key) or osw_session_end.  < 0: the window's own PCM,
+     * used for this window only. */
+    int64_t clip;
 } osw_session_window;
 int osw_session_begin(osw_ctx* ctx, const osw_decode_opts* opts);
 /* Queue n windows; window i reads clip pcm[offsets[i], offsets[i+1]) (host int16, copied). */
@@ -250,6 +256,9 @@ int osw_session_add(osw_ctx* ctx, const int16_t* pcm, const int64_t* offsets, in
  * *n_active / *n_queued: windows decoding / waiting after the call. */
 int osw_session_step(osw_ctx* ctx, int32_t max_chunks, int32_t refill_min, osw_window_result* res,
                      int64_t* tags_out, int32_t cap, int32_t* n_done, int32_t* n_active, int32_t* n_queued);
+/* Frees the resident log-mel of clip `clip` (no queued window may still read it; windows
+ * already admitted were staged and are unaffected). */
+int osw_session_release_clip(osw_ctx* ctx, int64_t clip);
 int osw_session_end(osw_ctx* ctx);
 
 /* Parity helper: one encoder block on x [T][D] fp32 (host), result to y (host). */

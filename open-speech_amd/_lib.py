@@ -47,7 +47,8 @@ class osw_window_result(C.Structure):
 
 class osw_session_window(C.Structure):
     _fields_ = [("tag", C.c_int64), ("seek", C.c_int32), ("segment_size", C.c_int32), ("language_token", C.c_int32),
-                ("token_budget", C.c_int32), ("n_prefix", C.c_int32), ("prefix", C.POINTER(C.c_int32))]
+                ("token_budget", C.c_int32), ("n_prefix", C.c_int32), ("prefix", C.POINTER(C.c_int32)),
+                ("clip", C.c_int64)]
 
 
 class osw_profile(C.Structure):
@@ -88,6 +89,7 @@ _SIGS = {
     "osw_session_add": (C.c_int, [C.c_void_p, C.c_void_p, P(C.c_int64), C.c_int32, P(osw_session_window)]),
     "osw_session_step": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, P(osw_window_result), P(C.c_int64), C.c_int32,
                                    P(C.c_int32), P(C.c_int32), P(C.c_int32)]),
+    "osw_session_release_clip": (C.c_int, [C.c_void_p, C.c_int64]),
     "osw_session_end": (C.c_int, [C.c_void_p]),
     "osw_encoder_layer_debug": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_float), P(C.c_float), C.c_int32]),
     "osw_debug_gemm": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,

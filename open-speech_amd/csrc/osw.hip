@@ -257,6 +257,7 @@ struct osw_ctx {
     int kv_rows = 0;                  // sessions: self-K/V cache rows per layer (0: the step's row count)
     int xkv_windows = 0;              // sessions: cross-K/V windows per layer (0: the step's windows)
     struct Session* sess = nullptr;   // an open decode session (osw_session_*)
+    struct ClipStore* cstore = nullptr;  // decode sessions' resident clip log-mels (created on first use)
     int* slot_d = nullptr;            // encode into slots: window -> decoder row
     int* refill_pack = nullptr;       // decode_refill: rows to admit {row, budget, prompt}
 
@@ -1547,9 +1548,34 @@ int64_t upfirdn_output_len(int64_t len_h, int64_t n_in, int64_t up, int64_t down
 // the rows up to the highest occupied slot.  Windows are admitted between chunks of CH steps:
 // their log-mel, their encoder straight into the slots' cross-K/V, then the rows' reset.
 struct SessionWin {
-    std::vector<int16_t> pcm;
+    int64_t clip;            // ClipStore key (a private key < 0 for a window that brought its own PCM)
     std::vector<int> prefix;
     osw_session_window w;
+};
+
+// The log-mel of every clip a decode session holds windows of, computed ONCE when the clip's
+// first window is added and kept on the device until the caller releases the clip
+// (osw_session_release_clip) or the session ends: a long file's later windows are staged
+// from it (a device-to-device copy of the window's frames and the clip's max) instead of
+// re-uploading the whole clip and recomputing its log-mel per window.  One
+// arena per context, first-fit spans, grown by doubling (the old contents keep their
+// offsets); per-clip maxima in a slot array.  Lives as long as the context.
+struct ClipStore {
+    struct Clip {
+        int64_t off = 0;   // first float of the clip's [nframes][n_mels] log10 mel in the arena
+        int nframes = 0;
+        int slot = 0;      // its max (ordered int) at maxv[slot]
+        bool priv = false; // registered for one window (no caller key): released at its admission
+    };
+    std::map<int64_t, Clip> clips;
+    int64_t next_priv = -2;
+    float* arena = nullptr;
+    int64_t cap = 0;                   // floats
+    std::map<int64_t, int64_t> spans;  // free spans: offset -> length (coalesced)
+    int* maxv = nullptr;
+    int slots_cap = 0;
+    std::vector<int> free_slots;
+    int64_t* hdr = nullptr;            // one clip's mel launch: pcm offsets {0, n}, mel_off {off, end}, nframes
 };
 struct Session {
     osw_decode_opts o{};
@@ -1563,6 +1589,122 @@ struct Session {
 
 namespace {
 using osw::SelState;
+
+ClipStore& clip_store(osw_ctx* c) {
+    if (!c->cstore) {
+        c->cstore = new ClipStore();
+        c->cstore->hdr = dalloc<int64_t>(6, c->owned);
+    }
+    return *c->cstore;
+}
+
+int64_t store_alloc(osw_ctx* c, ClipStore& cs, int64_t len) {
+    for (auto it = cs.spans.begin(); it != cs.spans.end(); ++it)
+        if (it->second >= len) {
+            const int64_t off = it->first, rest = it->second - len;
+            cs.spans.erase(it);
+            if (rest) cs.spans[off + len] = rest;
+            return off;
+        }
+    // grow: a bigger arena holding the old one's contents at the same offsets
+    const int64_t ncap = std::max<int64_t>(std::max<int64_t>(2 * cs.cap, cs.cap + len),
+                                           (int64_t)std::max(4, c->B) * 3001 * c->d.n_mels);
+    float* na = dalloc<float>((size_t)ncap, c->owned);
+    if (cs.arena) {
+        HIPCHK(hipMemcpyAsync(na, cs.arena, (size_t)cs.cap * 4, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        dfree(cs.arena, c->owned);
+    }
+    int64_t tail_off = cs.cap, tail_len = ncap - cs.cap;
+    if (!cs.spans.empty()) {
+        auto last = std::prev(cs.spans.end());
+        if (last->first + last->second == cs.cap) {
+            tail_off = last->first;
+            tail_len += last->second;
+            cs.spans.erase(last);
+        }
+    }
+    cs.arena = na;
+    cs.cap = ncap;
+    cs.spans[tail_off + len] = tail_len - len;
+    if (tail_len == len) cs.spans.erase(tail_off + len);
+    return tail_off;
+}
+
+void store_free(ClipStore& cs, int64_t off, int64_t len) {
+    auto it = cs.spans.emplace(off, len).first;
+    if (it != cs.spans.begin()) {
+        auto prev = std::prev(it);
+        if (prev->first + prev->second == off) {
+            prev->second += it->second;
+            cs.spans.erase(it);
+            it = prev;
+        }
+    }
+    auto next = std::next(it);
+    if (next != cs.spans.end() && it->first + it->second == next->first) {
+        it->second += next->second;
+        cs.spans.erase(next);
+    }
+}
+
+// Registers a clip: its PCM uploaded and its log-mel computed into the store (on the stream)
+void store_add(osw_ctx* c, int64_t key, const int16_t* pcm, int64_t n, bool priv) {
+    ClipStore& cs = clip_store(c);
+    REQUIRE(n >= 0, "bad clip length");
+    const int n_mels = c->d.n_mels;
+    ClipStore::Clip cl;
+    cl.nframes = (int)((n + 160) / 160);
+    cl.priv = priv;
+    cl.off = store_alloc(c, cs, (int64_t)cl.nframes * n_mels);
+    if (cs.free_slots.empty()) {
+        const int ncap = std::max(64, 2 * cs.slots_cap);
+        int* nm = dalloc<int>(ncap, c->owned);
+        if (cs.maxv) {
+            HIPCHK(hipMemcpyAsync(nm, cs.maxv, (size_t)cs.slots_cap * 4, hipMemcpyDeviceToDevice, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            dfree(cs.maxv, c->owned);
+        }
+        for (int i = ncap - 1; i >= cs.slots_cap; --i) cs.free_slots.push_back(i);
+        cs.maxv = nm;
+        cs.slots_cap = ncap;
+    }
+    cl.slot = cs.free_slots.back();
+    cs.free_slots.pop_back();
+    if ((size_t)n > c->pcm_cap) {
+        c->pcm_cap = (size_t)n + (size_t)n / 2 + 1;
+        dfree(c->pcm, c->owned);
+        c->pcm = dalloc<int16_t>(c->pcm_cap, c->owned);
+    }
+    if (n) HIPCHK(hipMemcpyAsync(c->pcm, pcm, (size_t)n * 2, hipMemcpyHostToDevice, c->stream));
+    const int64_t h[6] = {0, n, cl.off, cl.off + (int64_t)cl.nframes * n_mels, cl.nframes, 0};
+    HIPCHK(hipMemcpyAsync(cs.hdr, h, sizeof(h), hipMemcpyHostToDevice, c->stream));
+    {
+        Timed t(c, CL_MEL, (double)n * 2 + (double)cl.nframes * n_mels * 4);
+        // (nframes as the low int of hdr[4]: little-endian)
+        launch_mel(c->pcm, cs.hdr, cs.hdr + 2, (const int*)(cs.hdr + 4), 1, cl.nframes, c->tw400, c->hann, c->flo,
+                   c->fcnt, c->foff, c->fw, n_mels, cs.arena, cs.maxv + cl.slot, c->stream);
+        HIPCHK(hipGetLastError());
+    }
+    cs.clips[key] = cl;
+}
+
+void store_release(osw_ctx* c, int64_t key) {
+    if (!c->cstore) return;
+    ClipStore& cs = *c->cstore;
+    auto it = cs.clips.find(key);
+    if (it == cs.clips.end()) return;
+    store_free(cs, it->second.off, (int64_t)it->second.nframes * c->d.n_mels);
+    cs.free_slots.push_back(it->second.slot);
+    cs.clips.erase(it);
+}
+
+void store_clear(osw_ctx* c) {
+    if (!c->cstore) return;
+    std::vector<int64_t> keys;
+    for (auto& kv : c->cstore->clips) keys.push_back(kv.first);
+    for (int64_t k : keys) store_release(c, k);
+}
 
 void session_begin(osw_ctx* c, const osw_decode_opts* o) {
     REQUIRE(o, "null decode options");
@@ -1623,6 +1765,7 @@ void session_begin(osw_ctx* c, const osw_decode_opts* o) {
 }
 
 void session_end(osw_ctx* c) {
+    store_clear(c);
     delete c->sess;
     c->sess = nullptr;
     c->row_pos = false;
@@ -1635,15 +1778,38 @@ void session_add(osw_ctx* c, const int16_t* pcm, const int64_t* offsets, int n, 
     Session* S = c->sess;
     REQUIRE(S, "no decode session open");
     REQUIRE(pcm && offsets && w && n >= 0, "null argument");
+    // every window is checked before any is queued or any clip registered
+    ClipStore& cs = clip_store(c);
+    std::map<int64_t, int64_t> fresh;  // caller keys registered by this call -> window index
     for (int i = 0; i < n; ++i) {
         REQUIRE(offsets[i + 1] >= offsets[i], "offsets must not decrease");
         REQUIRE(w[i].segment_size >= 1 && w[i].seek >= 0, "empty window");
         REQUIRE(w[i].n_prefix >= 0 && (w[i].n_prefix == 0 || w[i].prefix), "bad prefix");
         REQUIRE(w[i].n_prefix + S->tail < S->max_len, "prompt longer than max_length");
+        int64_t samples = offsets[i + 1] - offsets[i];
+        if (w[i].clip >= 0) {
+            auto it = cs.clips.find(w[i].clip);
+            if (it != cs.clips.end()) {
+                samples = -1;
+                REQUIRE(w[i].seek < it->second.nframes, "window seek out of range");
+            } else if (fresh.count(w[i].clip)) {
+                samples = offsets[fresh[w[i].clip] + 1] - offsets[fresh[w[i].clip]];
+            } else {
+                fresh[w[i].clip] = i;
+            }
+        }
         // (log_mel's frame count: one frame per 160 samples, plus one)
-        REQUIRE(w[i].seek < (int)((offsets[i + 1] - offsets[i] + 160) / 160), "window seek out of range");
+        if (samples >= 0) REQUIRE(w[i].seek < (int)((samples + 160) / 160), "window seek out of range");
+    }
+    for (int i = 0; i < n; ++i) {
         SessionWin q;
-        q.pcm.assign(pcm + offsets[i], pcm + offsets[i + 1]);
+        if (w[i].clip >= 0) {
+            if (!cs.clips.count(w[i].clip)) store_add(c, w[i].clip, pcm + offsets[i], offsets[i + 1] - offsets[i], false);
+            q.clip = w[i].clip;
+        } else {
+            q.clip = cs.next_priv--;
+            store_add(c, q.clip, pcm + offsets[i], offsets[i + 1] - offsets[i], true);
+        }
         q.prefix.assign(w[i].prefix, w[i].prefix + w[i].n_prefix);
         q.w = w[i];
         q.w.prefix = nullptr;
@@ -1660,21 +1826,56 @@ void session_admit(osw_ctx* c, int refill_min) {
     if (!queued || free_slots.empty()) return;
     if (S->active > 0 && (int)free_slots.size() < std::min(std::max(1, refill_min), queued)) return;
     const int k = std::min((int)free_slots.size(), queued);
-    std::vector<int16_t> pcm;
-    std::vector<int64_t> offs(k + 1, 0);
-    for (int i = 0; i < k; ++i) {
-        pcm.insert(pcm.end(), S->queue[i].pcm.begin(), S->queue[i].pcm.end());
-        offs[i + 1] = (int64_t)pcm.size();
+    // the admitted windows' frames, staged from their clips' resident log-mel as k "clips"
+    // (window i = its frames [seek, seek + min(segment, frames - seek)) and its clip's max), so
+    // encode() sees the layout log_mel() writes
+    ClipStore& cs = clip_store(c);
+    const int n_mels = c->d.n_mels;
+    if (k > c->clips_cap) {
+        const int cap = std::max(k, 2 * c->clips_cap);
+        dfree(c->offsets, c->owned);
+        dfree(c->mel_off_d, c->owned);
+        dfree(c->nframes_d, c->owned);
+        dfree(c->clip_max, c->owned);
+        c->offsets = dalloc<int64_t>(cap + 1, c->owned);
+        c->mel_off_d = dalloc<int64_t>(cap + 1, c->owned);
+        c->nframes_d = dalloc<int>(cap, c->owned);
+        c->clip_max = dalloc<int>(cap, c->owned);
+        c->clips_cap = cap;
     }
-    if (pcm.empty()) pcm.push_back(0);
-    log_mel(c, pcm.data(), offs.data(), k, 0, nullptr);
+    c->nframes.assign(k, 0);
+    c->mel_off.assign(k + 1, 0);
+    std::vector<int64_t> src_off(k);
+    std::vector<int> src_slot(k);
+    for (int i = 0; i < k; ++i) {
+        const SessionWin& q = S->queue[i];
+        const ClipStore::Clip& cl = cs.clips.at(q.clip);
+        const int len = std::max(1, std::min(std::min(q.w.segment_size, N_FR), cl.nframes - q.w.seek));
+        c->nframes[i] = len;
+        c->mel_off[i + 1] = c->mel_off[i] + (int64_t)len * n_mels;
+        src_off[i] = cl.off + (int64_t)q.w.seek * n_mels;
+        src_slot[i] = cl.slot;
+    }
+    if ((size_t)c->mel_off[k] > c->logmel_cap) {
+        c->logmel_cap = (size_t)c->mel_off[k] + (size_t)c->mel_off[k] / 2;
+        dfree(c->logmel, c->owned);
+        c->logmel = dalloc<float>(c->logmel_cap, c->owned);
+    }
+    for (int i = 0; i < k; ++i) {
+        HIPCHK(hipMemcpyAsync(c->logmel + c->mel_off[i], cs.arena + src_off[i],
+                              (size_t)(c->mel_off[i + 1] - c->mel_off[i]) * 4, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(c->clip_max + i, cs.maxv + src_slot[i], 4, hipMemcpyDeviceToDevice, c->stream));
+    }
+    HIPCHK(hipMemcpyAsync(c->mel_off_d, c->mel_off.data(), (k + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->nframes_d, c->nframes.data(), k * 4, hipMemcpyHostToDevice, c->stream));
+    c->n_clips = k;
     const int ps = 3 + S->ctx;
     std::vector<osw_window> wins(k);
     std::vector<int> slots(k), pack((size_t)k * ps, 0);
     for (int i = 0; i < k; ++i) {
         const SessionWin& q = S->queue[i];
         const int slot = free_slots[i];
-        wins[i] = osw_window{i, q.w.seek, q.w.segment_size};
+        wins[i] = osw_window{i, 0, q.w.segment_size};
         slots[i] = slot;
         int* e = &pack[(size_t)i * ps];
         const int np = (int)q.prefix.size();
@@ -1693,7 +1894,10 @@ void session_admit(osw_ctx* c, int refill_min) {
     launch_session_rows(c->refill_pack, k, ps, S->beam, S->ctx, S->ctx, c->prompt, c->budget, c->cur_tok, c->pos,
                         c->sel, S->beam > 1 ? c->anc : nullptr, S->beam > 1 ? c->bwin : nullptr, c->stream);
     HIPCHK(hipGetLastError());
-    for (int i = 0; i < k; ++i) S->queue.pop_front();
+    for (int i = 0; i < k; ++i) {
+        if (S->queue.front().clip < 0) store_release(c, S->queue.front().clip);  // (its frames were staged)
+        S->queue.pop_front();
+    }
     S->active += k;
 }
 
@@ -1920,6 +2124,8 @@ int osw_destroy(osw_ctx* c) {
             for (auto& kv : c->dgraphs) (void)hipGraphExecDestroy(kv.second.first);
             delete c->sess;
             c->sess = nullptr;
+            delete c->cstore;
+            c->cstore = nullptr;
             for (void* p : c->owned) (void)hipFree(p);
             if (c->done_host) (void)hipHostFree(c->done_host);
             destroy_streams(c);
@@ -2136,6 +2342,18 @@ int osw_session_step(osw_ctx* c, int32_t max_chunks, int32_t refill_min, osw_win
         *n_active = c->sess->active;
         *n_queued = (int32_t)c->sess->queue.size();
         resolve_events(c);
+    });
+}
+
+int osw_session_release_clip(osw_ctx* c, int64_t clip) {
+    return guard([&] {
+        REQUIRE(c, "null ctx");
+        std::lock_guard<std::mutex> lk(c->mu);
+        REQUIRE(c->sess, "no decode session open");
+        REQUIRE(clip >= 0, "clip keys are >= 0");
+        for (const SessionWin& q : c->sess->queue)
+            REQUIRE(q.clip != clip, "a queued window still reads this clip");
+        store_release(c, clip);
     });
 }
 

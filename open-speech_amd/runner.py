@@ -278,7 +278,12 @@ class _SessionLane(_Worker):
         added = False           # windows queued since the last admission
 
         def answer(t, exc=None):
-            req, s, _ = flights.pop(t)
+            req, s, w = flights.pop(t)
+            if w is not None and is_open:
+                try:
+                    eng.session_release_clip(t)   # the request's resident log-mel
+                except Exception:  # noqa: BLE001 - best effort; session_end frees it anyway
+                    pass
             if not req.fut.done():
                 if exc is None and s is not None:
                     req.fut.set_result(finish_clip(s, req.opts, tok))
@@ -291,7 +296,9 @@ class _SessionLane(_Worker):
                 answer(t)
                 return
             w = next_window(s, req.opts, tok)
-            w.update(tag=t, pcm=req.pcm)
+            # the request's clip key is its tag: the first window brings the PCM (its log-mel
+            # is computed once and stays on the device), later windows only the key
+            w.update(tag=t, clip=t, pcm=req.pcm if flights[t][2] is None else None)
             flights[t][2] = w
             eng.session_add([w])
             nonlocal added

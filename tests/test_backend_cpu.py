@@ -64,10 +64,18 @@ class FakeEngine:
         self.sessions = getattr(self, "sessions", 0) + 1
 
     def session_add(self, wins):
+        clips = self._sess.setdefault("clips", {})
         for w in wins:
-            if w["seek"] >= len(w["pcm"]) // 160 + 1:
+            if w.get("pcm") is not None and w.get("clip") not in clips:
+                clips[w.get("clip")] = len(w["pcm"])
+            n = clips[w["clip"]] if w.get("clip") is not None else len(w["pcm"])
+            if w["seek"] >= n // 160 + 1:
                 raise ValueError("window seek out of range")
             self._sess["q"].append(w)
+
+    def session_release_clip(self, clip):
+        self._sess.get("clips", {}).pop(clip, None)
+        self.released = getattr(self, "released", 0) + 1
 
     def session_step(self, max_chunks=1, refill_min=1):
         time.sleep(getattr(self, "step_sleep", 0.0))

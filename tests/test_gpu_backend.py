@@ -312,6 +312,7 @@ def test_backend_continuous_matches_oracle_seek_loop(monkeypatch, tmp_path):
         def __init__(self, eng):
             self.eng = eng
             self.tags = {}
+            self.clip_hash = {}
 
         def __getattr__(self, k):
             return getattr(self.eng, k)
@@ -326,7 +327,10 @@ def test_backend_continuous_matches_oracle_seek_loop(monkeypatch, tmp_path):
         def session_add(self, wins):
             with lock:
                 for w in wins:
-                    h = hashlib.sha1(np.asarray(w["pcm"], np.int16).tobytes()).hexdigest()
+                    # a request's first window brings its PCM; later ones only its clip key
+                    if w.get("pcm") is not None:
+                        self.clip_hash[w["clip"]] = hashlib.sha1(np.asarray(w["pcm"], np.int16).tobytes()).hexdigest()
+                    h = self.clip_hash[w["clip"]]
                     self.tags[w["tag"]] = (h, w["seek"], w["segment_size"])
                     added[(h, w["seek"], w["segment_size"])] = list(w["prefix"] or [])
             return self.eng.session_add(wins)

@@ -175,3 +175,113 @@ def test_session_end_midway_then_new_session():
         _compare(eng, cfg, wins[:6], got)
     finally:
         eng.close()
+
+
+def test_session_clip_keys_match_own_pcm():
+    """Resident clip log-mels (osw_session_window::clip, ADVICE r5): the windows of a 95 s
+    clip and a 47 s clip queued by key — PCM with each clip's first window only, later
+    windows staged from the clip's log-mel kept on the device — decode exactly as the same
+    windows queued with their own PCM, and as each window alone.  A released key needs its
+    PCM again."""
+    d = D.TINY_TEST
+    st = SpecialTokens.for_vocab(d.n_vocab)
+    eng = WhisperEngine(d, device=0, max_batch=3)
+    try:
+        eng.load_weights(weights.random_weights(d, seed=99, emb_std=0.5))
+        sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+        cfg = DecodeConfig(suppress_tokens=sup, max_length=48, beam_size=1)
+        long_, mid = synth.chirp_clip(901, 95.0), synth.chirp_clip(902, 47.0)
+        wins = []
+        for key, pcm, seeks in ((7, long_, (0, 2900, 5600, 8100, 9300)), (8, mid, (0, 1800, 4000))):
+            nf = len(pcm) // 160 + 1
+            for j, sk in enumerate(seeks):
+                wins.append(dict(tag=100 * key + j, clip=key, pcm=pcm if j == 0 else None, seek=sk,
+                                 segment_size=min(3000, nf - 1 - sk), language_token=st.first_lang,
+                                 prefix=[st.sot_prev, 300 + j] if j else None, token_budget=6 + 3 * j))
+        own = [dict(w, clip=None, pcm=long_ if w["tag"] < 800 else mid) for w in wins]
+        got_key = _run_session(eng, cfg, wins, add_in=(0.4, 0.7, 1.0))
+        got_own = _run_session(eng, cfg, own, add_in=(0.4, 0.7, 1.0))
+        for w in wins:
+            a, b = got_key[w["tag"]], got_own[w["tag"]]
+            assert (a.tokens, a.sum_logprob, a.no_speech_prob, a.language) == \
+                (b.tokens, b.sum_logprob, b.no_speech_prob, b.language), w["tag"]
+        _compare(eng, cfg, own, got_key)
+        # a key is forgotten after release (and after session_end): its windows need PCM again
+        eng.session_begin(cfg)
+        try:
+            eng.session_add([wins[0]])
+            eng.session_release_clip(7)
+            with pytest.raises(Exception):
+                eng.session_add([dict(wins[1])])
+        finally:
+            eng.session_end()
+    finally:
+        eng.close()
+
+
+def test_session_long_clip_admission_does_not_grow():
+    """The per-window admission cost of a 20-minute clip's later windows (staged from its
+    resident log-mel) is not the whole-clip upload + log-mel it was: it stays
+    within a small factor of a 30 s clip's."""
+    import time
+
+    import numpy as np
+    d = D.TINY_TEST
+    st = SpecialTokens.for_vocab(d.n_vocab)
+    eng = WhisperEngine(d, device=0, max_batch=2)
+    try:
+        eng.load_weights(weights.random_weights(d, seed=5, emb_std=0.5))
+        sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+        cfg = DecodeConfig(suppress_tokens=sup, max_length=24)
+        eng.session_begin(cfg)
+        try:
+            def admit(key, pcm, seek, first):
+                t = time.perf_counter()
+                eng.session_add([dict(tag=key * 1000 + seek, clip=key, pcm=pcm if first else None, seek=seek,
+                                      segment_size=3000, language_token=st.first_lang, token_budget=2)])
+                eng.session_step(max_chunks=0)
+                dt = time.perf_counter() - t
+                while True:
+                    _, active, queued = eng.session_step(max_chunks=4)
+                    if active == 0 and queued == 0:
+                        return dt
+            long_ = np.tile(synth.chirp_clip(11, 60.0), 20)          # 20 minutes
+            short = synth.chirp_clip(12, 30.5)
+            admit(1, long_, 0, True)
+            admit(2, short, 0, True)
+            t_long = min(admit(1, long_, s, False) for s in (30000, 60000, 90000))
+            t_short = min(admit(2, short, 0, False) for _ in range(3))
+            print(f"admission: 20-min clip's later window {t_long * 1e3:.2f} ms, 30 s clip's {t_short * 1e3:.2f} ms")
+            assert t_long < 3.0 * t_short + 2e-3, (t_long, t_short)
+        finally:
+            eng.session_end()
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("beam", [1, 5])
+def test_session_near_prompt_limits(beam):
+    """the per-row prompt path near its limits — max_length 448 (the runner's),
+    a <|startofprev|> prefix of 223 tokens (the seek loop's cap, 448 // 2 - 1, plus
+    <|startofprev|>), windows that run to max_length (no budget) beside short ones: every
+    window equals its decode alone (SelState::plen, pstride = n_text_ctx, beam lseq/lanc)."""
+    d = D.TINY_TEST
+    st = SpecialTokens.for_vocab(d.n_vocab)
+    eng = WhisperEngine(d, device=0, max_batch=3)
+    try:
+        eng.load_weights(weights.random_weights(d, seed=31, emb_std=0.5))
+        sup = get_suppressed_tokens(WhisperTokenizer(d.n_vocab), [-1])
+        cfg = DecodeConfig(suppress_tokens=sup, max_length=448, beam_size=beam)
+        wins = []
+        for i in range(4):
+            pcm = synth.chirp_clip(950 + i, 30.0)
+            n_pre = (223, 223, 40, 0)[i]
+            prefix = [st.sot_prev] + [200 + (17 * i + 5 * j) % 400 for j in range(n_pre)] if n_pre else None
+            wins.append(dict(tag=i, pcm=pcm, seek=0, segment_size=3000, language_token=st.first_lang + i,
+                             prefix=prefix, token_budget=(0, 12, 0, 30)[i]))
+        got = _run_session(eng, cfg, wins, add_in=(0.5, 1.0))
+        _compare(eng, cfg, wins, got)
+        print("near-limit windows: prompt", [len(w["prefix"] or []) + 3 for w in wins], "sampled",
+              [len(got[w["tag"]].tokens) for w in wins])
+    finally:
+        eng.close()

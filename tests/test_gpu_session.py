@@ -209,10 +209,13 @@ def test_session_clip_keys_match_own_pcm():
         # a key is forgotten after release (and after session_end): its windows need PCM again
         eng.session_begin(cfg)
         try:
-            eng.session_add([wins[0]])
+            eng.session_add([wins[0], dict(wins[1])])
+            with pytest.raises(Exception, match="queued window"):
+                eng.session_release_clip(7)             # a queued window still reads it
+            eng.session_step(max_chunks=0)              # both admitted (staged from the clip)
             eng.session_release_clip(7)
-            with pytest.raises(Exception):
-                eng.session_add([dict(wins[1])])
+            with pytest.raises(Exception, match="seek out of range"):
+                eng.session_add([dict(wins[2])])        # key 7 is gone and this window has no PCM
         finally:
             eng.session_end()
     finally:

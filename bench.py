@@ -86,7 +86,7 @@ def parse(argv=None):
     ap.add_argument("--realistic-steps", type=int, default=9,
                     help="also time this many steps with realistic output lengths (random weights never emit "
                          "<|endoftext|>: each clip's length is forced from a seeded distribution)")
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r05_fin5_pmc.json"),
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r06_f_pmc.json"),
                     help="per-kernel HBM bytes from a rocprofv3 --pmc pass (tools/pmc_summary.py)")
     ap.add_argument("--standin", action="store_true",
                     help="launcher test only: ranks run a CPU stand-in engine over gloo (no GPU, no HIP library)")
@@ -640,7 +640,8 @@ def main(argv=None):
             "beam5_audio_sec_per_sec_1lane": beam5,
             "realtime_factor": round(value, 1),
             "roofline": roof,
-            "rooflines": {k: {kk: v[kk] for kk in ("achieved", "unit", "frac", "avg_launch_ms")} for k, v in roofs.items()},
+            "rooflines": {k: {kk: v[kk] for kk in ("achieved", "unit", "frac", "avg_launch_ms", "valu") if kk in v}
+                          for k, v in roofs.items()},
             "stages_ms_roofline_pass": stages,
             "decode_steps_last_call": int(profs[0]["decode_steps"]),
             "cpu_baseline": cpu,

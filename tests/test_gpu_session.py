@@ -225,7 +225,7 @@ def test_session_clip_keys_match_own_pcm():
 def test_session_long_clip_admission_does_not_grow():
     """The per-window admission cost of a 20-minute clip's later windows (staged from its
     resident log-mel) is not the whole-clip upload + log-mel it was: it stays
-    within a small factor of a 30 s clip's."""
+    within a small factor of a 30 s clip's (timings printed with -s)."""
     import time
 
     import numpy as np
@@ -255,7 +255,9 @@ def test_session_long_clip_admission_does_not_grow():
             t_long = min(admit(1, long_, s, False) for s in (30000, 60000, 90000))
             t_short = min(admit(2, short, 0, False) for _ in range(3))
             print(f"admission: 20-min clip's later window {t_long * 1e3:.2f} ms, 30 s clip's {t_short * 1e3:.2f} ms")
-            assert t_long < 3.0 * t_short + 2e-3, (t_long, t_short)
+            # (before the resident log-mel each later window re-uploaded 38 MB and recomputed the
+            # 20-minute clip's 120 000-frame log-mel; the bound leaves room for timing noise)
+            assert t_long < 4.0 * t_short + 5e-3, (t_long, t_short)
         finally:
             eng.session_end()
     finally:

@@ -228,13 +228,18 @@ class _SessionLane(_Worker):
                         # call) and then takes everything that queued meanwhile — the lanes
                         # take turns on the encoder
                         if not idle:
-                            return ("sess", key, [])
-                        if deadline is None:
+                            # a busy lane keeps decoding — unless a request has waited
+                            # max_pace_ms already (then it is admitted beside the encoder)
+                            waited = time.monotonic() - dq.items[0].t_enq
+                            if not pool.busy_admit or waited < pool.max_pace_ms / 1000.0:
+                                return ("sess", key, [])
+                        elif deadline is None:
                             deadline = time.monotonic() + pool.max_pace_ms / 1000.0
-                        left = deadline - time.monotonic()
-                        if left > 0:
-                            dq.cv.wait(timeout=left)
-                            continue
+                        if idle:
+                            left = deadline - time.monotonic()
+                            if left > 0:
+                                dq.cv.wait(timeout=left)
+                                continue
                         # waited max_pace_ms: take requests beside the running encoder
                     if idle:
                         head = dq.items[0]
@@ -416,6 +421,10 @@ class BatchRunner:
         self.continuous = continuous
         self.refill_min = refill_min
         self.spread_ms = spread_ms
+        # a busy session lane admits a request that waited max_pace_ms even while another lane
+        # encodes; STT_HIP_BUSY_ADMIT=0: never (the round-5 pacing, for A/B runs)
+        import os
+        self.busy_admit = os.environ.get("STT_HIP_BUSY_ADMIT", "1") != "0"
         self._sup_cache: dict = {}
         self._lock = threading.Lock()
         self.queues: list[_DevQueue] = []

@@ -775,6 +775,63 @@ def test_capture_error_is_not_a_device_fault():
         runner.close()
 
 
+@pytest.mark.parametrize("busy_admit", ["1", "0"])
+def test_busy_lane_admits_a_request_that_waited(monkeypatch, busy_admit):
+    """while another lane of the GPU encodes, a busy session lane keeps decoding
+    instead of admitting — but a request that has waited max_pace_ms is admitted by the
+    busy lane beside the running encoder (STT_HIP_BUSY_ADMIT=0: it waits for the encoder)."""
+    from concurrent.futures import Future
+    from open_speech_amd.runner import BatchRunner, _Req
+    from open_speech_amd.segments import TranscribeOptions
+    from open_speech_amd.tokenizer import WhisperTokenizer
+
+    monkeypatch.setenv("STT_HIP_BUSY_ADMIT", busy_admit)
+    slow_admit = threading.Event()
+
+    class Eng(FakeEngine):
+        def session_step(self, max_chunks=1, refill_min=1):
+            if max_chunks == 0 and self.tag == "slow" and slow_admit.is_set():
+                time.sleep(0.6)          # a long encoder on this lane
+            return super().session_step(max_chunks, refill_min)
+
+    busy, slow = Eng(D.MICRO_TEST, 0, 4), Eng(D.MICRO_TEST, 0, 4)
+    busy.device = slow.device = 0                # two lanes of one GPU: one queue, one encoder count
+    busy.tag, slow.tag = "busy", "slow"
+    busy.step_sleep = slow.step_sleep = 0.005
+    # spread_ms: the busy lane leaves a fresh request to the idle sibling (which then encodes)
+    runner = BatchRunner([busy, slow], WhisperTokenizer(51866), continuous=True, max_pace_ms=50, spread_ms=1000)
+    try:
+        opts = TranscribeOptions(language="en")
+        long_req = _Req(synth.chirp_clip(1, 300.0), opts, Future())   # keeps one lane busy (10 windows)
+        runner.submit_req(long_req)
+        deadline = time.monotonic() + 5
+        while not (busy.batches or slow.batches) and time.monotonic() < deadline:
+            time.sleep(0.002)
+        busy_eng = busy if busy.batches else slow
+        other = slow if busy_eng is busy else busy
+        other.tag, busy_eng.tag = "slow", "busy"
+        busy_eng.step_sleep = 0.1                # its 10 windows keep it busy for seconds
+        slow_admit.set()
+        first = _Req(synth.chirp_clip(2, 3.0), opts, Future())
+        runner.submit_req(first)                 # the idle lane takes it and encodes slowly
+        time.sleep(0.05)
+        t0 = time.monotonic()
+        late = _Req(synth.chirp_clip(3, 3.0), opts, Future())
+        runner.submit_req(late)
+        late.fut.result(timeout=10)
+        waited = time.monotonic() - t0
+        busy_still = not long_req.fut.done()
+        if busy_admit == "1":
+            assert waited < 0.45, waited          # admitted by the busy lane after ~max_pace_ms
+        else:
+            assert waited > 0.45, waited          # only after the slow encoder finished
+        first.fut.result(timeout=10)
+        assert busy_still                        # the other lane was busy throughout
+        long_req.fut.result(timeout=30)
+    finally:
+        runner.close()
+
+
 def test_session_lane_close_drains_flights():
     """closing the runner (unload_model) lets a session lane finish the requests
     it is decoding instead of failing them with 'runner closed'."""

@@ -81,11 +81,21 @@ __device__ __forceinline__ void store_one(const GemmArgs& g, int m, int n, float
     }
 }
 
+// An accumulator's epilogue value, v + bias (hb: the GEMM has a bias), GELU'd for fc1
+// (EPI_F32_GELU_POS: GELU + pos in the copy-out pass, fewer live registers).  The tile
+// epilogues load the bias of a thread's columns into registers ONCE per tile: loading
+// g.bias[n] per accumulator (rounds 1-5) re-loaded it behind every LDS image write (generic
+// pointers: the compiler could not prove they do not alias, so it kept no value) and waited
+// for each load with a full vmcnt(0) — 256-336 load/wait pairs per 8-phase tile epilogue in
+// the ISA.  With no bias the register holds -0.0f, the exact additive identity of IEEE
+// round-to-nearest (x + -0 == x for every x, -0 included), so the add is unconditional —
+// a select on "has bias" was hoisted by the compiler across the passes and spilled.  Same
+// arithmetic, bit for bit.
 template <int EPI>
-__device__ __forceinline__ float epi_value(const GemmArgs& g, int m, int n, float v) {
-    if (g.bias) v += g.bias[n];
+__device__ __forceinline__ float epi_apply(float v, float b) {
+    v += b;
     if constexpr (EPI == EPI_F16_GELU) v = gelu_erf(v);
-    return v;  // EPI_F32_GELU_POS: GELU + pos applied in the copy-out pass (fewer live registers)
+    return v;
 }
 
 // LDS-staged epilogue of a TM x TM tile held as 2 x 2 waves of (TM/2)^2 (gemm_kernel,
@@ -99,6 +109,10 @@ __device__ __forceinline__ void staged_epilogue_sq(const GemmArgs& g, const f32x
     static_assert(EPI != EPI_F32, "plain fp32 tiles keep their write-through element stores");
     constexpr int FT = TM / 32, WT = TM / 2;
     const int lane = tid & 63;
+    const bool hb = g.bias != nullptr;
+    float bs[FT];  // the bias of this thread's FT columns, loaded once (epi_apply)
+#pragma unroll
+    for (int ni = 0; ni < FT; ++ni) bs[ni] = hb ? g.bias[min(n0 + wn * WT + ni * 16 + (lane & 15), g.N - 1)] : -0.f;
     if constexpr (EPI == EPI_F16 || EPI == EPI_F16_GELU || EPI == EPI_HEADS) {
         h16* T = (h16*)smem;
         auto at = [](int row, int col) { return row * TM + ((((col >> 3) ^ row) & (TM / 8 - 1)) << 3) + (col & 7); };
@@ -110,7 +124,7 @@ __device__ __forceinline__ void staged_epilogue_sq(const GemmArgs& g, const f32x
                 for (int i = 0; i < 4; ++i) {
                     const int row = wm * WT + mi * 16 + (lane >> 4) * 4 + i;
                     const int col = wn * WT + ni * 16 + (lane & 15);
-                    T[at(row, col)] = (h16)epi_value<EPI>(g, m0 + row, min(n0 + col, g.N - 1), acc[mi][ni][i]);
+                    T[at(row, col)] = (h16)epi_apply<EPI>(acc[mi][ni][i], bs[ni]);
                 }
         __syncthreads();
 #pragma unroll 4
@@ -141,23 +155,35 @@ __device__ __forceinline__ void staged_epilogue_sq(const GemmArgs& g, const f32x
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int row = wm * WT + mi * 16 + (lane >> 4) * 4 + i;
-                    const int col = wn * WT + ni * 16 + (lane & 15);
-                    T[at(row, col)] = epi_value<EPI>(g, m0 + row, min(n0 + col, g.N - 1), acc[mi][ni][i]);
+                    T[at(row, wn * WT + ni * 16 + (lane & 15))] = epi_apply<EPI>(acc[mi][ni][i], bs[ni]);
                 }
         __syncthreads();
-#pragma unroll 4
-        for (int j = 0; j < TM * TM / 4 / NTHR; ++j) {
+        // the residual (or positional) operands of every piece this thread stores are loaded
+        // before any is used: one round trip, not one per piece
+        constexpr int NJ = TM * TM / 4 / NTHR;
+        f32x4 aux[EPI == EPI_F32_RESID || EPI == EPI_F32_GELU_POS ? NJ : 1];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int id = j * NTHR + tid;
+            const int row = id / (TM / 4), c4 = (id % (TM / 4)) * 4;
+            const int m = min(m0 + row, g.M - 1), n = min(n0 + c4, g.N - 4);
+            if constexpr (EPI == EPI_F32_RESID)
+                aux[j] = *(const f32x4*)((float*)g.C + (m / g.c_grp_rows) * g.c_grp_stride +
+                                         (int64_t)(m % g.c_grp_rows) * g.ldc + n);
+            if constexpr (EPI == EPI_F32_GELU_POS) aux[j] = *(const f32x4*)&g.pos[(int64_t)(m % g.c_grp_rows) * g.N + n];
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
             const int id = j * NTHR + tid;
             const int row = id / (TM / 4), c4 = (id % (TM / 4)) * 4;
             const int m = m0 + row, n = n0 + c4;
             if (m >= g.M || n >= g.N) continue;
             f32x4 val = *(const f32x4*)&T[at(row, c4)];
             float* dst = (float*)g.C + (m / g.c_grp_rows) * g.c_grp_stride + (int64_t)(m % g.c_grp_rows) * g.ldc + n;
-            if constexpr (EPI == EPI_F32_RESID) val += *(const f32x4*)dst;
+            if constexpr (EPI == EPI_F32_RESID) val += aux[j];
             if constexpr (EPI == EPI_F32_GELU_POS) {
-                const f32x4 pv = *(const f32x4*)&g.pos[(int64_t)(m % g.c_grp_rows) * g.N + n];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) val[e] = gelu_erf(val[e]) + pv[e];
+                for (int e = 0; e < 4; ++e) val[e] = gelu_erf(val[e]) + aux[j][e];
             }
             *(f32x4*)dst = val;
         }
@@ -327,6 +353,22 @@ template <int EPI, bool IL = false, bool TR = false>
 __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], int m0, int n0, int wm,
                                                 int wn, char* smem, int tid) {
     const int lane = tid & 63;
+    // the bias of this thread's columns, loaded once per tile (epi_apply): TR, 4 columns per
+    // accumulator block (one 16-B load each); otherwise one column per block
+    // (fp32 forms: one f32x4 per thread, added at copy-out, whose columns are fixed per thread)
+    constexpr bool F16 = EPI == EPI_F16 || EPI == EPI_F16_GELU || EPI == EPI_HEADS;
+    const bool hb = g.bias != nullptr;
+    f32x4 bt[4];
+    float bs[4];
+#pragma unroll
+    for (int ni = 0; ni < 4 && F16; ++ni) {
+        if constexpr (TR) {
+            const int n = min(n0 + acc_col<IL>(wn, ni) + 4 * (lane >> 4), g.N - 4);
+            bt[ni] = hb ? *(const f32x4*)(g.bias + n) : f32x4{-0.f, -0.f, -0.f, -0.f};
+        } else {
+            bs[ni] = hb ? g.bias[min(n0 + acc_col<IL>(wn, ni) + (lane & 15), g.N - 1)] : -0.f;
+        }
+    }
     __syncthreads();
     if constexpr (EPI == EPI_F16 || EPI == EPI_F16_GELU || EPI == EPI_HEADS) {
         // IL (every wave holds rows of both 128-row halves): the tile leaves in two halves,
@@ -344,10 +386,9 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
                     if (IL && (mi >> 2) != half) continue;
                     const int row = acc_row<IL>(wm, mi) + (lane & 15);
                     const int col = acc_col<IL>(wn, ni) + 4 * (lane >> 4);
-                    const int n = min(n0 + col, g.N - 4);
                     h16x4 v;
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] = (h16)epi_value<EPI>(g, m0 + row, n + e, acc[mi][ni][e]);
+                    for (int e = 0; e < 4; ++e) v[e] = (h16)epi_apply<EPI>(acc[mi][ni][e], bt[ni][e]);
                     *(h16x4*)&T[ep16(row, col)] = v;
                 }
         } else
@@ -360,8 +401,7 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
                     if (IL && (mi >> 2) != half) continue;
                     const int row = acc_row<IL>(wm, mi) + (lane >> 4) * 4 + i;
                     const int col = acc_col<IL>(wn, ni) + (lane & 15);
-                    const int n = min(n0 + col, g.N - 1);
-                    T[ep16(row, col)] = (h16)epi_value<EPI>(g, m0 + row, n, acc[mi][ni][i]);
+                    T[ep16(row, col)] = (h16)epi_apply<EPI>(acc[mi][ni][i], bs[ni]);
                 }
         __syncthreads();
 #pragma unroll 4
@@ -385,6 +425,9 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
         }
     } else {
         float* T = (float*)smem;
+        // this thread's 4 copy-out columns are the same in every piece (GNT % 64 == 0)
+        const f32x4 b4 = hb ? *(const f32x4*)(g.bias + min(n0 + (tid & 63) * 4, g.N - 4))
+                            : f32x4{-0.f, -0.f, -0.f, -0.f};
         for (int half = 0; half < 2; ++half) {
             if (IL || wm == half) {
 #pragma unroll
@@ -396,28 +439,47 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
                             if (IL && (mi >> 2) != half) continue;
                             const int row = acc_row<IL>(wm, mi) - half * 128 + (lane >> 4) * 4 + i;
                             const int col = acc_col<IL>(wn, ni) + (lane & 15);
-                            const int n = min(n0 + col, g.N - 1);
-                            T[ep32(row, col)] = epi_value<EPI>(g, m0 + half * 128 + row, n, acc[mi][ni][i]);
+                            T[ep32(row, col)] = acc[mi][ni][i];
                         }
             }
             __syncthreads();
-#pragma unroll 4
-            for (int j = 0; j < 16; ++j) {
+            // the residual (positional) operands of AB pieces in flight at once: 16 / AB round
+            // trips per half instead of one per piece (each piece's load was followed by a full
+            // vmcnt(0) wait, which also waited for the previous piece's store).  AB = 8 when
+            // only the other half's accumulators are live (IL); 1 when all are (more spilled).
+            constexpr int AB = IL ? 8 : 1;
+#pragma unroll
+            for (int j0 = 0; j0 < 16; j0 += AB) {
+            f32x4 aux[EPI == EPI_F32_RESID || EPI == EPI_F32_GELU_POS ? AB : 1];
+#pragma unroll
+            for (int jj = 0; jj < AB; ++jj) {
+                const int id = (j0 + jj) * GNT + tid;
+                const int row = id >> 6, c4 = (id & 63) * 4;
+                const int m = min(m0 + half * 128 + row, g.M - 1), n = min(n0 + c4, g.N - 4);
+                if constexpr (EPI == EPI_F32_RESID)
+                    aux[jj] = *(const f32x4*)((float*)g.C + (m / g.c_grp_rows) * g.c_grp_stride +
+                                              (int64_t)(m % g.c_grp_rows) * g.ldc + n);
+                if constexpr (EPI == EPI_F32_GELU_POS)
+                    aux[jj] = *(const f32x4*)&g.pos[(int64_t)(m % g.c_grp_rows) * g.N + n];
+            }
+#pragma unroll
+            for (int jj = 0; jj < AB; ++jj) {
+                const int j = j0 + jj;
                 const int id = j * GNT + tid;
                 const int row = id >> 6, c4 = (id & 63) * 4;
                 const int m = m0 + half * 128 + row, n = n0 + c4;
                 if (m < g.M && n < g.N) {
-                    f32x4 v = *(const f32x4*)&T[ep32(row, c4)];
+                    f32x4 v = *(const f32x4*)&T[ep32(row, c4)] + b4;
                     float* dst = (float*)g.C + (m / g.c_grp_rows) * g.c_grp_stride +
                                  (int64_t)(m % g.c_grp_rows) * g.ldc + n;
-                    if constexpr (EPI == EPI_F32_RESID) v += *(const f32x4*)dst;
+                    if constexpr (EPI == EPI_F32_RESID) v += aux[jj];
                     if constexpr (EPI == EPI_F32_GELU_POS) {
-                        const f32x4 pv = *(const f32x4*)&g.pos[(int64_t)(m % g.c_grp_rows) * g.N + n];
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]) + pv[e];
+                        for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]) + aux[jj][e];
                     }
                     __builtin_nontemporal_store(v, (f32x4*)dst);
                 }
+            }
             }
             __syncthreads();
         }
@@ -585,6 +647,19 @@ __device__ __forceinline__ void staged_epilogue_next0(const GemmArgs& g, f32x4 (
     constexpr bool F16 = EPI == EPI_F16 || EPI == EPI_F16_GELU || EPI == EPI_HEADS;
     constexpr int PR = F16 ? 128 : 64;       // image rows per pass
     constexpr int NP = 256 / PR;
+    // the bias of this thread's columns, loaded once per tile (epi_apply; see staged_epilogue)
+    const bool hb = g.bias != nullptr;
+    f32x4 bt[4];
+    float bs[4];
+#pragma unroll
+    for (int ni = 0; ni < 4 && F16; ++ni) {
+        if constexpr (TR) {
+            const int n = min(n0 + acc_col<true>(wn, ni) + 4 * (lane >> 4), g.N - 4);
+            bt[ni] = hb ? *(const f32x4*)(g.bias + n) : f32x4{-0.f, -0.f, -0.f, -0.f};
+        } else {
+            bs[ni] = hb ? g.bias[min(n0 + acc_col<true>(wn, ni) + (lane & 15), g.N - 1)] : -0.f;
+        }
+    }
     lds_sync();  // every wave is past its last read of buffer 1 (the last K-tile's)
 #pragma unroll
     for (int pass = 0; pass < NP; ++pass) {
@@ -598,11 +673,9 @@ __device__ __forceinline__ void staged_epilogue_next0(const GemmArgs& g, f32x4 (
                         if ((mi >> 2) != pass) continue;
                         const int row = acc_row<true>(wm, mi) - pass * PR + (lane & 15);
                         const int col = acc_col<true>(wn, ni) + 4 * (lane >> 4);
-                        const int n = min(n0 + col, g.N - 4);
                         h16x4 v;
 #pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            v[e] = (h16)epi_value<EPI>(g, m0 + pass * PR + row, n + e, acc[mi][ni][e]);
+                        for (int e = 0; e < 4; ++e) v[e] = (h16)epi_apply<EPI>(acc[mi][ni][e], bt[ni][e]);
                         *(h16x4*)&T[ep16(row, col)] = v;
                     }
             } else
@@ -615,8 +688,7 @@ __device__ __forceinline__ void staged_epilogue_next0(const GemmArgs& g, f32x4 (
                         if ((mi >> 2) != pass) continue;
                         const int row = acc_row<true>(wm, mi) - pass * PR + (lane >> 4) * 4 + i;
                         const int col = acc_col<true>(wn, ni) + (lane & 15);
-                        const int n = min(n0 + col, g.N - 1);
-                        T[ep16(row, col)] = (h16)epi_value<EPI>(g, m0 + pass * PR + row, n, acc[mi][ni][i]);
+                        T[ep16(row, col)] = (h16)epi_apply<EPI>(acc[mi][ni][i], bs[ni]);
                     }
             lds_sync();
 #pragma unroll 4
@@ -639,6 +711,8 @@ __device__ __forceinline__ void staged_epilogue_next0(const GemmArgs& g, f32x4 (
             }
         } else {
             float* T = (float*)(smem + 4 * HT * 2);
+            const f32x4 b4 = hb ? *(const f32x4*)(g.bias + min(n0 + (tid & 63) * 4, g.N - 4))
+                                : f32x4{-0.f, -0.f, -0.f, -0.f};
             // pass p = rows [64 p, 64 p + 64): wave rows (mi >> 2) * 128 + wm * 64
             if (wm == (pass & 1)) {
 #pragma unroll
@@ -650,26 +724,41 @@ __device__ __forceinline__ void staged_epilogue_next0(const GemmArgs& g, f32x4 (
                             if ((mi >> 2) != (pass >> 1)) continue;
                             const int row = acc_row<true>(wm, mi) - pass * PR + (lane >> 4) * 4 + i;
                             const int col = acc_col<true>(wn, ni) + (lane & 15);
-                            const int n = min(n0 + col, g.N - 1);
-                            T[ep32(row, col)] = epi_value<EPI>(g, m0 + pass * PR + row, n, acc[mi][ni][i]);
+                            T[ep32(row, col)] = acc[mi][ni][i];
                         }
             }
             lds_sync();
-#pragma unroll 4
-            for (int j = 0; j < 8; ++j) {
-                const int id = j * GNT + tid;
-                const int row = id >> 6, c4 = (id & 63) * 4;
-                const int m = m0 + pass * PR + row, n = n0 + c4;
-                if (m < g.M && n < g.N) {
-                    f32x4 v = *(const f32x4*)&T[ep32(row, c4)];
-                    float* dst = (float*)g.C + (m / g.c_grp_rows) * g.c_grp_stride + (int64_t)(m % g.c_grp_rows) * g.ldc + n;
-                    if constexpr (EPI == EPI_F32_RESID) v += *(const f32x4*)dst;
-                    if constexpr (EPI == EPI_F32_GELU_POS) {
-                        const f32x4 pv = *(const f32x4*)&g.pos[(int64_t)(m % g.c_grp_rows) * g.N + n];
+            // the residual (positional) operands in flight 4 at a time: every accumulator is
+            // still live here (later passes), so 8 at a time spilled
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]) + pv[e];
+            for (int j0 = 0; j0 < 8; j0 += 4) {
+                f32x4 aux[EPI == EPI_F32_RESID || EPI == EPI_F32_GELU_POS ? 4 : 1];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const int id = (j0 + jj) * GNT + tid;
+                    const int row = id >> 6, c4 = (id & 63) * 4;
+                    const int m = min(m0 + pass * PR + row, g.M - 1), n = min(n0 + c4, g.N - 4);
+                    if constexpr (EPI == EPI_F32_RESID)
+                        aux[jj] = *(const f32x4*)((float*)g.C + (m / g.c_grp_rows) * g.c_grp_stride +
+                                                  (int64_t)(m % g.c_grp_rows) * g.ldc + n);
+                    if constexpr (EPI == EPI_F32_GELU_POS)
+                        aux[jj] = *(const f32x4*)&g.pos[(int64_t)(m % g.c_grp_rows) * g.N + n];
+                }
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const int id = (j0 + jj) * GNT + tid;
+                    const int row = id >> 6, c4 = (id & 63) * 4;
+                    const int m = m0 + pass * PR + row, n = n0 + c4;
+                    if (m < g.M && n < g.N) {
+                        f32x4 v = *(const f32x4*)&T[ep32(row, c4)] + b4;
+                        float* dst = (float*)g.C + (m / g.c_grp_rows) * g.c_grp_stride + (int64_t)(m % g.c_grp_rows) * g.ldc + n;
+                        if constexpr (EPI == EPI_F32_RESID) v += aux[jj];
+                        if constexpr (EPI == EPI_F32_GELU_POS) {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]) + aux[jj][e];
+                        }
+                        __builtin_nontemporal_store(v, (f32x4*)dst);
                     }
-                    __builtin_nontemporal_store(v, (f32x4*)dst);
                 }
             }
         }

@@ -805,7 +805,10 @@ __device__ __forceinline__ void gemm8p_tile(const GemmArgs& g, int bid, h16* sme
     for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    h16x8 af[4][2], bf[2][2];
+    // KW (DBG 3, 4): W0's fragments stay in registers (bw) from phase 1 to phase 4
+    constexpr bool KW = DBG == 3 || DBG == 4;
+    constexpr bool NOEPI = DBG == 1 || DBG == 4;
+    h16x8 af[4][2], bf[2][2], bw[KW ? 2 : 1][2];
 
     auto read_a = [&](const h16* hb) {
 #pragma unroll
@@ -821,12 +824,19 @@ __device__ __forceinline__ void gemm8p_tile(const GemmArgs& g, int bid, h16* sme
             bf[nt][1] = *(const h16x8*)&hb[boff1 + nt * 16 * BK];
         }
     };
+    auto read_w0 = [&](const h16* hb) {
+#pragma unroll
+        for (int nt = 0; nt < (KW ? 2 : 0); ++nt) {
+            bw[nt][0] = *(const h16x8*)&hb[boff0 + nt * 16 * BK];
+            bw[nt][1] = *(const h16x8*)&hb[boff1 + nt * 16 * BK];
+        }
+    };
     auto barrier = [] {
         asm volatile("" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     };
-    auto mfma = [&](int a, int b) {
+    auto mfma_with = [&](int a, int b, const h16x8 (&B)[2][2]) {
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
@@ -834,18 +844,82 @@ __device__ __forceinline__ void gemm8p_tile(const GemmArgs& g, int bid, h16* sme
             for (int nt = 0; nt < 2; ++nt) {
                 f32x4 c = acc[a * 4 + mt][b * 2 + nt];
                 if constexpr (TR) {  // transposed: Cᵀ = W Aᵀ, the same products in the same K order
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[nt][0], af[mt][0], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[nt][1], af[mt][1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(B[nt][0], af[mt][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(B[nt][1], af[mt][1], c, 0, 0, 0);
                 } else {
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mt][0], bf[nt][0], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mt][1], bf[nt][1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mt][0], B[nt][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mt][1], B[nt][1], c, 0, 0, 0);
                 }
                 acc[a * 4 + mt][b * 2 + nt] = c;
             }
         __builtin_amdgcn_s_setprio(0);
     };
+    auto mfma = [&](int a, int b) { mfma_with(a, b, bf); };
 
     const int nk = g.K / BK;
+    if constexpr (KW) {
+        // Issue order per K-tile t: phase 1 W1(t+1), 2 A1(t+1), 3 A0(t+2), 4 W0(t+2); every
+        // half-tile slot is restaged 2-3 phases after its last read (W0's last read is phase 1)
+        // and waited for 4 phases after its issue (vmcnt(8): the 4 younger half-tiles stay in
+        // flight), in the phase before the one that reads it:
+        //   phase 1 retires W1(t) (read in 2), 2 A1(t) (read in 3), 4 A0(t+1) + W0(t+1).
+        // (The default order re-reads W0 in phase 4, which holds W0(t+1)'s restage back to
+        // phase 2 and leaves it 2 phases to arrive.)
+        if (!pre0) {
+            stage(0, 0);
+            stage(2, 0);
+            stage(3, 0);
+            stage(1, 0);
+        }
+        if (nk > 1) {
+            stage(0, 1);
+            stage(2, 1);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        }
+        barrier();
+        if (__builtin_amdgcn_readfirstlane(wave) >= 4) barrier();  // group 1 runs one barrier behind group 0
+        for (int t = 0; t < nk; ++t) {
+            const h16* buf = smem + (t & 1) * 4 * HT;
+            const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
+            // phase 1: quadrant (0,0) from A0, W0 (W0 kept)
+            if (n1) stage(3, t + 1);
+            read_a(buf + 0 * HT);
+            read_w0(buf + 2 * HT);
+            if (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            barrier();
+            mfma_with(0, 0, bw);
+            barrier();
+            // phase 2: quadrant (0,1) from W1
+            if (n1) stage(1, t + 1);
+            read_b(buf + 3 * HT);
+            if (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            barrier();
+            mfma(0, 1);
+            barrier();
+            // phase 3: quadrant (1,1) from A1
+            if (n2) stage(0, t + 2);
+            read_a(buf + 1 * HT);
+            barrier();
+            mfma(1, 1);
+            barrier();
+            // phase 4: quadrant (1,0), no reads
+            if (n2) {
+                stage(2, t + 2);
+                asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            } else if (n1) {
+                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            barrier();
+            mfma_with(1, 0, bw);
+            barrier();
+        }
+    } else {
     // prologue = phases 3, 4 of tile -2 and tile -1 in the steady-state order
     if (!pre0) {
         stage(0, 0);
@@ -897,6 +971,7 @@ __device__ __forceinline__ void gemm8p_tile(const GemmArgs& g, int bid, h16* sme
         mfma(1, 0);
         barrier();
     }
+    }
     if (__builtin_amdgcn_readfirstlane(wave) < 4) barrier();
     if (next_bid >= 0) {
         // every wave is past its reads of buffer 0 (the last K-tile read buffer 1: nk even):
@@ -904,16 +979,18 @@ __device__ __forceinline__ void gemm8p_tile(const GemmArgs& g, int bid, h16* sme
         lds_sync();
         int nm0, nn0;
         tile8p_origin(g, next_bid, nm0, nn0);
+        // (the prologue's issue order: A0 W1 A1 W0, KW: A0 W0 W1 A1)
+        constexpr int H0 = 0, H1 = KW ? 2 : 3, H2 = KW ? 3 : 1, H3 = KW ? 1 : 2;
 #pragma unroll
-        for (int H : {0, 3, 1, 2})
+        for (int H : {H0, H1, H2, H3})
 #pragma unroll
             for (int i = 0; i < 2; ++i)
                 __builtin_amdgcn_global_load_lds((const void*)src8p(g, nm0, nn0, H, i, wave, lane),
                                                  (OSW_LDS void*)(smem + H * HT + (i * 8 + wave) * 8 * BK), 16, 0, 0);
-        if constexpr (DBG != 1) staged_epilogue_next0<EPI, TR>(g, acc, m0, n0, wm, wn, (char*)smem, tid);
+        if constexpr (!NOEPI) staged_epilogue_next0<EPI, TR>(g, acc, m0, n0, wm, wn, (char*)smem, tid);
         return;
     }
-    if constexpr (DBG == 1) {
+    if constexpr (NOEPI) {
         float t = 0.f;
 #pragma unroll
         for (int i = 0; i < 8; ++i)
@@ -2128,6 +2205,14 @@ void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s) {
     }
     if (variant == 10) {
         launch8p<EPI_F16_GELU>(g, s);
+        return;
+    }
+    if (variant == 14) {  // debug: the KW loop (W0 kept in registers), no epilogue / fp16 out
+        launch8p<EPI_F32, 4>(g, s);
+        return;
+    }
+    if (variant == 15) {
+        launch8p<EPI_F16, 3>(g, s);
         return;
     }
     if (variant == 12 || variant == 13) {  // debug: fp16 / GELU epilogues on accumulators not transposed

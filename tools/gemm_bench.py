@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
-"""Time the GEMM variants on the encoder / decoder shapes (GPU)."""
+"""Time the GEMM variants on the encoder / decoder shapes (GPU).
+
+usage: gemm_bench.py [shape-prefix] [variants]"""
 import json
 import os
 import sys
@@ -28,17 +30,24 @@ eng = WhisperEngine(d, device=0, max_batch=1)
 rng = np.random.default_rng(0)
 out = []
 only = sys.argv[1] if len(sys.argv) > 1 else ""
+# optional comma (or colon) list of variants overriding each shape's own (e.g. 9,8,10,4: the 8-phase
+# kernel with no epilogue / fp16 out / GELU fp16 out / fp32 out)
+force = tuple(int(v) for v in sys.argv[2].replace(":", ",").split(",")) if len(sys.argv) > 2 else None
 for name, M, N, K, vs in SHAPES:
     if only and not name.startswith(only):
         continue
     A = rng.uniform(-1, 1, (M, K)).astype(np.float16)
     W = rng.uniform(-1, 1, (N, K)).astype(np.float16)
-    for v in vs:
-        _, ms = eng.debug_gemm(A, W, v, iters=5)
+    first = None
+    for v in force or vs:
+        C, ms = eng.debug_gemm(A, W, v, iters=5)
+        if first is None:
+            first = C
+        same = bool(np.array_equal(C.view(np.uint32), first.view(np.uint32)))
         tf = 2.0 * M * N * K / (ms * 1e-3) / 1e12
         gbs = (N * K * 2 + M * K * 2 + M * N * 4) / (ms * 1e-3) / 1e9
         r = {"shape": name, "M": M, "N": N, "K": K, "variant": v, "ms": round(ms, 4), "TFLOPs": round(tf, 1),
-             "GBs": round(gbs, 1)}
+             "GBs": round(gbs, 1), "bits_equal_first": same}
         out.append(r)
         print(json.dumps(r), flush=True)
 eng.close()

@@ -41,7 +41,7 @@ __device__ __forceinline__ h16x4 ds_read_tr(const h16* p) {
 // fp16 P operand); O and l stay relative to the same stale max, so the normalised result
 // is the same softmax, and the 32 O rescale multiplies per tile run only when some lane
 // of the wave raised its max (rare after the first tiles) instead of every tile.
-template <bool LAZY, int QT>
+template <bool LAZY, int QT, bool PIPE>
 __device__ __forceinline__ void enc_attn_unit(const h16* __restrict__ qkv, h16* __restrict__ out, int T, int H,
                                               int nb, int nqb, int nwg, int bid, h16 (&lds)[2][2][KB * HD]) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -68,17 +68,16 @@ __device__ __forceinline__ void enc_attn_unit(const h16* __restrict__ qkv, h16* 
     }
 
     // glds pieces: 64 rows x 128 B = 8 KiB per tile = 8 wave-instructions; K: 2 per wave, V: 2 per wave
-    auto stage = [&](int buf, int k0) {
+    auto stage_part = [&](int buf, int part, int k0) {
+        const h16* src = part ? Vh : Kh;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int piece = i * 4 + wave;           // rows piece*8 .. +7
             const int r = piece * 8 + (lane >> 3);
             const int c = swz(r, lane & 7);
             const int key = min(k0 + r, T - 1);
-            __builtin_amdgcn_global_load_lds((const void*)(Kh + (int64_t)key * HD + c * 8),
-                                             (OSW_LDS void*)&lds[buf][0][piece * 8 * HD], 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((const void*)(Vh + (int64_t)key * HD + c * 8),
-                                             (OSW_LDS void*)&lds[buf][1][piece * 8 * HD], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)(src + (int64_t)key * HD + c * 8),
+                                             (OSW_LDS void*)&lds[buf][part][piece * 8 * HD], 16, 0, 0);
         }
     };
 
@@ -96,22 +95,9 @@ __device__ __forceinline__ void enc_attn_unit(const h16* __restrict__ qkv, h16* 
         for (int dt = 0; dt < 4; ++dt) o[qt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const int nkt = (T + KB - 1) / KB;
-    stage(0, 0);
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    // one K/V tile; TAIL: the last one, whose keys past T are masked (a separate
-    // instantiation: the masking selects cost ~50 VALU ops per tile in every tile when the
-    // condition was a runtime flag, in a VALU-bound loop)
-    auto tile = [&](int kt, auto tail_c) {
-        constexpr bool tail = decltype(tail_c)::value;
-        const int buf = kt & 1;
-        if (kt + 1 < nkt) stage(buf ^ 1, (kt + 1) * KB);
-        const h16* Kl = lds[buf][0];
-        const h16* Vl = lds[buf][1];
-        const int k0 = kt * KB;
 
-        // ---- Sᵀ = K Qᵀ : sc[qt][t] holds keys 16t + 4g + i for query li
-        f32x4 sc[QT][4];
+    // ---- Sᵀ = K Qᵀ : sc[qt][t] holds keys 16t + 4g + i for query li
+    auto qk = [&](const h16* Kl, f32x4 (&sc)[QT][4]) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int row = 16 * t + li;
@@ -125,11 +111,19 @@ __device__ __forceinline__ void enc_attn_unit(const h16* __restrict__ qkv, h16* 
                 sc[qt][t] = a;
             }
         }
-        // ---- online softmax (lane-local per query; 4 lanes g=0..3 share a query).  VALU
-        // is this loop's bound at d = 64 (≈ 2x the MFMA cycles), so: the running max is
-        // kept on raw scores and the 1/sqrt(d)*log2(e) scale folds into one FMA per score,
-        // keys past T are masked only in the last tile, and exp2 is the bare v_exp_f32
-        // (results below 2^-126 flush to 0, irrelevant next to the row maximum's 1).
+    };
+    // ---- online softmax of tile kt's scores, then Oᵀ += Vᵀ Pᵀ.  TAIL: the last tile,
+    // whose keys past T are masked (a separate instantiation: the masking selects cost ~50
+    // VALU ops per tile in every tile when the condition was a runtime flag, in a VALU-bound
+    // loop)
+    auto softmax_pv = [&](int kt, auto tail_c, f32x4 (&sc)[QT][4], const h16* Vl) {
+        constexpr bool tail = decltype(tail_c)::value;
+        const int k0 = kt * KB;
+        // (lane-local per query; 4 lanes g=0..3 share a query).  VALU is this loop's bound
+        // at d = 64 (≈ 2x the MFMA cycles), so: the running max is kept on raw scores and
+        // the 1/sqrt(d)*log2(e) scale folds into one FMA per score, keys past T are masked
+        // only in the last tile, and exp2 is the bare v_exp_f32 (results below 2^-126 flush
+        // to 0, irrelevant next to the row maximum's 1).
         h16x8 pf[QT][2];
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) {
@@ -157,12 +151,18 @@ __device__ __forceinline__ void enc_attn_unit(const h16* __restrict__ qkv, h16* 
             const float mcs = -mnew * cs;
             float ls = 0.f;
             float p[4][4];
+            // the scale + shift of two scores per packed FMA (v_pk_fma_f32: the same fused
+            // multiply-add per element as fmaf, half the issue slots in this VALU-bound loop)
+            const f32x2 cs2 = {cs, cs}, mcs2 = {mcs, mcs};
 #pragma unroll
             for (int t = 0; t < 4; ++t)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    p[t][i] = __builtin_amdgcn_exp2f(fmaf(sc[qt][t][i], cs, mcs));
+                for (int i = 0; i < 4; i += 2) {
+                    const f32x2 x = __builtin_elementwise_fma(f32x2{sc[qt][t][i], sc[qt][t][i + 1]}, cs2, mcs2);
+                    p[t][i] = __builtin_amdgcn_exp2f(x.x);
                     ls += p[t][i];
+                    p[t][i + 1] = __builtin_amdgcn_exp2f(x.y);
+                    ls += p[t][i + 1];
                 }
             lrun[qt] = lrun[qt] * alpha + ls;
             if (rescale) {
@@ -203,12 +203,70 @@ __device__ __forceinline__ void enc_attn_unit(const h16* __restrict__ qkv, h16* 
                     o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf[qt][s], o[qt][dt], 0, 0, 0);
             }
         }
-        __builtin_amdgcn_s_waitcnt(0);
-        __syncthreads();
     };
     const bool last_partial = nkt * KB > T;
-    for (int kt = 0; kt < nkt - (last_partial ? 1 : 0); ++kt) tile(kt, std::false_type{});
-    if (last_partial) tile(nkt - 1, std::true_type{});
+    if constexpr (!PIPE) {
+        // one K/V tile per step, the next tile's K and V staged at its start
+        stage_part(0, 0, 0);
+        stage_part(0, 1, 0);
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        auto tile = [&](int kt, auto tail_c) {
+            const int buf = kt & 1;
+            if (kt + 1 < nkt) {
+                stage_part(buf ^ 1, 0, (kt + 1) * KB);
+                stage_part(buf ^ 1, 1, (kt + 1) * KB);
+            }
+            f32x4 sc[QT][4];
+            qk(lds[buf][0], sc);
+            softmax_pv(kt, tail_c, sc, lds[buf][1]);
+            __builtin_amdgcn_s_waitcnt(0);
+            __syncthreads();
+        };
+        for (int kt = 0; kt < nkt - (last_partial ? 1 : 0); ++kt) tile(kt, std::false_type{});
+        if (last_partial) tile(nkt - 1, std::true_type{});
+    } else {
+        // Software-pipelined (PIPE): step kt computes tile kt+1's scores (MFMA) in the same
+        // block as tile kt's softmax (VALU) and PV (MFMA), so one wave's matrix and vector
+        // work interleave instead of taking turns.  K(j) lives in lds[j & 1][0] and V(j) in
+        // lds[j & 1][1]; step kt stages K(kt+2) into the K half its own scores came from and
+        // V(kt+1) into the V half tile kt-1's PV read, both free after the previous step's
+        // barrier, and reads K(kt+1) and V(kt), both landed before it.  The same MFMAs and
+        // softmax per tile in the same order as the unpipelined form: identical results.
+        stage_part(0, 0, 0);
+        stage_part(0, 1, 0);
+        if (nkt > 1) stage_part(1, 0, KB);
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        f32x4 sa[QT][4], sb[QT][4];
+        qk(lds[0][0], sa);
+        auto step = [&](int kt, auto tail_c, auto next_c, f32x4 (&cur)[QT][4], f32x4 (&nxt)[QT][4]) {
+            constexpr bool next = decltype(next_c)::value;
+            const int buf = kt & 1;
+            if (kt + 2 < nkt) stage_part(buf, 0, (kt + 2) * KB);
+            if (kt + 1 < nkt) stage_part(buf ^ 1, 1, (kt + 1) * KB);
+            if constexpr (next) qk(lds[buf ^ 1][0], nxt);
+            softmax_pv(kt, tail_c, cur, lds[buf][1]);
+            __builtin_amdgcn_s_waitcnt(0);
+            __syncthreads();
+        };
+        // steps 0 .. nkt-2 have a next tile; the roles of sa / sb alternate (unrolled by 2,
+        // so no register copies)
+        int kt = 0;
+        for (; kt + 1 < nkt - 1; kt += 2) {
+            step(kt, std::false_type{}, std::true_type{}, sa, sb);
+            step(kt + 1, std::false_type{}, std::true_type{}, sb, sa);
+        }
+        if (kt < nkt - 1) {
+            step(kt, std::false_type{}, std::true_type{}, sa, sb);
+            ++kt;
+            if (last_partial) step(kt, std::true_type{}, std::false_type{}, sb, sa);
+            else step(kt, std::false_type{}, std::false_type{}, sb, sa);
+        } else {
+            if (last_partial) step(kt, std::true_type{}, std::false_type{}, sa, sb);
+            else step(kt, std::false_type{}, std::false_type{}, sa, sb);
+        }
+    }
 
     // ---- normalise and store: lane holds O[q = li][d = 16 dt + 4 g + i]
     const int D = H * HD;
@@ -238,13 +296,13 @@ __device__ __forceinline__ void enc_attn_unit(const h16* __restrict__ qkv, h16* 
 // windows, where 128-query blocks leave CUs idle: 240 workgroups at one window).  A
 // query's arithmetic does not depend on the queries beside it (the lazy max is per lane;
 // a skipped rescale is a multiply by exactly 1), so both forms give identical results.
-template <bool LAZY, int QT>
+template <bool LAZY, int QT, bool PIPE>
 __global__ __launch_bounds__(256, 2) void enc_attn_kernel(const h16* __restrict__ qkv, h16* __restrict__ out,
                                                           int T, int H, int nb, int nqb) {
     __shared__ __attribute__((aligned(16))) h16 lds[2][2][KB * HD];  // [buf][K|V] 32 KiB
     const int nwg = nqb * H * nb;
     for (int vb = blockIdx.x; vb < nwg; vb += gridDim.x) {
-        enc_attn_unit<LAZY, QT>(qkv, out, T, H, nb, nqb, nwg, vb, lds);
+        enc_attn_unit<LAZY, QT, PIPE>(qkv, out, T, H, nb, nqb, nwg, vb, lds);
         __syncthreads();  // the LDS ring is the next unit's
     }
 }
@@ -271,13 +329,19 @@ void launch_enc_attn(const h16* qkv, h16* out, int T, int H, int nb, hipStream_t
         return 1 << 30;
     }();
     const int grid = std::min(nwg, cap);
+    static const bool pipe = [] {  // OSW_ATTN_PIPE=1: the software-pipelined step (A/B)
+        const char* e = std::getenv("OSW_ATTN_PIPE");
+        return e && e[0] == '1';
+    }();
+#define OSW_ATTN_LAUNCH(L, Q, P) enc_attn_kernel<L, Q, P><<<grid, 256, 0, s>>>(qkv, out, T, H, nb, nqb)
     if (small) {
-        if (eager) enc_attn_kernel<false, 1><<<grid, 256, 0, s>>>(qkv, out, T, H, nb, nqb);
-        else enc_attn_kernel<true, 1><<<grid, 256, 0, s>>>(qkv, out, T, H, nb, nqb);
+        if (eager) pipe ? OSW_ATTN_LAUNCH(false, 1, true) : OSW_ATTN_LAUNCH(false, 1, false);
+        else pipe ? OSW_ATTN_LAUNCH(true, 1, true) : OSW_ATTN_LAUNCH(true, 1, false);
     } else {
-        if (eager) enc_attn_kernel<false, 2><<<grid, 256, 0, s>>>(qkv, out, T, H, nb, nqb);
-        else enc_attn_kernel<true, 2><<<grid, 256, 0, s>>>(qkv, out, T, H, nb, nqb);
+        if (eager) pipe ? OSW_ATTN_LAUNCH(false, 2, true) : OSW_ATTN_LAUNCH(false, 2, false);
+        else pipe ? OSW_ATTN_LAUNCH(true, 2, true) : OSW_ATTN_LAUNCH(true, 2, false);
     }
+#undef OSW_ATTN_LAUNCH
 }
 
 }  // namespace osw

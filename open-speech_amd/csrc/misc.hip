@@ -3,6 +3,8 @@
 // weight init (bit-identical to open-speech_amd/weights.py:hash_uniform).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace osw {
 
 namespace {
@@ -44,6 +46,47 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
     }
 }
 
+// D % 256 == 0 (base and up; tiny's 384 takes the float2 kernel above): 16-B loads of the
+// residual, gamma and beta, 8-B fp16 stores (the float2 form moved 737 MB per turbo encoder
+// LayerNorm at ≈ 5.0 TB/s: ten 512-B wave-loads per row and 256-B wave-stores)
+template <int PER>  // PER = D / 256 float4 per lane
+__global__ __launch_bounds__(256) void layernorm4_kernel(const float* __restrict__ x, int64_t M, int D,
+                                                         const float* __restrict__ g, const float* __restrict__ b,
+                                                         h16* __restrict__ y) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= M) return;
+    const f32x4* xr = (const f32x4*)(x + row * D);
+    f32x4 v[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) v[i] = __builtin_nontemporal_load(&xr[i * 64 + lane]);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    const float mean = wave_sum(s) / D;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const f32x4 a = v[i] - mean;
+        q += (a.x * a.x + a.y * a.y) + (a.z * a.z + a.w * a.w);
+    }
+    const float rstd = rsqrtf(wave_sum(q) / D + 1e-5f);
+    const f32x4* g4 = (const f32x4*)g;
+    const f32x4* b4 = (const f32x4*)b;
+    h16x4* yr = (h16x4*)(y + row * D);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int c = i * 64 + lane;
+        const f32x4 gg = g4[c], bb = b4[c];
+        h16x4 o;
+        o[0] = (h16)((v[i].x - mean) * rstd * gg.x + bb.x);
+        o[1] = (h16)((v[i].y - mean) * rstd * gg.y + bb.y);
+        o[2] = (h16)((v[i].z - mean) * rstd * gg.z + bb.z);
+        o[3] = (h16)((v[i].w - mean) * rstd * gg.w + bb.w);
+        __builtin_nontemporal_store(o, &yr[c]);
+    }
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -71,6 +114,19 @@ __global__ void f16_to_f32_kernel(const h16* __restrict__ a, float* __restrict__
 
 void launch_layernorm(const float* x, int64_t M, int D, const float* g, const float* b, h16* y, hipStream_t s) {
     const dim3 grid((unsigned)((M + 3) / 4));
+    static const bool f2 = [] {  // OSW_LN_F2=1: the float2 kernel at every width (A/B)
+        const char* e = std::getenv("OSW_LN_F2");
+        return e && e[0] == '1';
+    }();
+    if (D % 256 == 0 && !f2) {
+        switch (D / 256) {
+            case 2: layernorm4_kernel<2><<<grid, 256, 0, s>>>(x, M, D, g, b, y); return;
+            case 3: layernorm4_kernel<3><<<grid, 256, 0, s>>>(x, M, D, g, b, y); return;
+            case 4: layernorm4_kernel<4><<<grid, 256, 0, s>>>(x, M, D, g, b, y); return;
+            case 5: layernorm4_kernel<5><<<grid, 256, 0, s>>>(x, M, D, g, b, y); return;
+            default: break;
+        }
+    }
     switch (D / 128) {
         case 1: layernorm_kernel<1><<<grid, 256, 0, s>>>(x, M, D, g, b, y); break;
         case 2: layernorm_kernel<2><<<grid, 256, 0, s>>>(x, M, D, g, b, y); break;

@@ -13,6 +13,7 @@
 #   b1          batch-1 greedy step breakdown               -> $O/b1_breakdown.txt
 #   b1beam      batch-1 beam-5 step breakdown               -> $O/b1beam_breakdown.txt
 #   pmcb1beam   SQ counter passes over a batch-1 beam-5 call -> $O/pmc_b1beam_{1,2}.txt
+#   pmcenc      the same SQ passes over one 64-window greedy step -> $O/pmc_enc_{1,2}.txt
 #   repro       tools/graph_prof_repro (mode 2) under a rocprofv3 kernel trace -> $O/repro.log
 #   bench:ARGS  bench.py with extra args (commas -> spaces) -> $O/bench_N.json
 #   py:SCRIPT,ARGS  python3 SCRIPT ARGS                     -> $O/py_N.txt
@@ -70,6 +71,17 @@ for s in "$@"; do
       rc=$?; [ $rc -eq 0 ] && python3 tools/b1_breakdown.py $O/b1bprof/run_kernel_trace.csv $((5*445)) > $O/b1beam_breakdown.txt && head -40 $O/b1beam_breakdown.txt
       [ $rc -eq 0 ] && python3 tools/step_timeline.py $O/b1bprof/run_kernel_trace.csv beam_update 1500 > $O/b1beam_step_timeline.txt && cat $O/b1beam_step_timeline.txt
       rm -f $O/b1bprof/run_kernel_trace.csv ;;
+    pmcenc)
+      # the same SQ counter passes over one 64-window greedy step (one lane)
+      for f in 1 2; do
+        CN=$(sed -e 's/^pmc: *//' tools/pmc_sq$f.txt)
+        timeout -s KILL 300 rocprofv3 --pmc $CN --output-format csv -d $O/pe$f -o run -- python3 bench.py --steps 1 --warmup 0 --lanes 1 --latency-repeats 0 --beam5-latency-repeats 0 --beam5 0 --beam5-steps 0 --realistic-steps 0 --stream-sessions 0 --rest-callers 0 --no-cpu-baseline > $O/pe$f.log 2>&1; rc=$?
+        CSV=$(find $O/pe$f -name '*counter_collection.csv' | head -1)
+        [ -n "$CSV" ] && python3 tools/pmc_generic.py $CSV > $O/pmc_enc_$f.txt
+        find $O/pe$f -name '*.csv' -delete
+        [ $rc -ne 0 ] && break
+      done
+      [ $rc -eq 0 ] && grep -A1 "enc_attn\|gemm8p" $O/pmc_enc_*.txt | head -40 ;;
     pmcb1beam)
       for f in 1 2; do
         CN=$(sed -e 's/^pmc: *//' tools/pmc_sq$f.txt)

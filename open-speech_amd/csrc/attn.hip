@@ -28,6 +28,13 @@ namespace {
 constexpr int QB = 128, KB = 64, HD = 64;
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+// V's chunk swizzle.  A half-wave's ds_read_b64_tr_b16 reads 8 consecutive rows (an aligned
+// 8-row group) x the two 16-B chunks {2dt, 2dt+1}; a 256-B bank row holds two 128-B rows, so
+// the 4 even (odd) rows need pairwise different chunk pairs: c ^ (row & 6) gives them pair
+// classes 0..3.  K's swizzle (row >> 1) gave rows 2n and 2n+2 the same pair: 2-way bank
+// conflicts on every V read (SQ_LDS_BANK_CONFLICT = a third of the kernel's LDS cycles,
+// profiles/r06_q_pmc_enc_1.txt).  Same bytes read, so identical results.
+__device__ __forceinline__ int swzv(int row, int chunk) { return chunk ^ (row & 6); }
 
 typedef __fp16 fp16x4_t __attribute__((__vector_size__(4 * sizeof(__fp16))));
 
@@ -74,7 +81,7 @@ __device__ __forceinline__ void enc_attn_unit(const h16* __restrict__ qkv, h16* 
         for (int i = 0; i < 2; ++i) {
             const int piece = i * 4 + wave;           // rows piece*8 .. +7
             const int r = piece * 8 + (lane >> 3);
-            const int c = swz(r, lane & 7);
+            const int c = part ? swzv(r, lane & 7) : swz(r, lane & 7);
             const int key = min(k0 + r, T - 1);
             __builtin_amdgcn_global_load_lds((const void*)(src + (int64_t)key * HD + c * 8),
                                              (OSW_LDS void*)&lds[buf][part][piece * 8 * HD], 16, 0, 0);
@@ -190,8 +197,8 @@ __device__ __forceinline__ void enc_attn_unit(const h16* __restrict__ qkv, h16* 
                 const int ch = col >> 3, within = col & 7;
                 const int r0 = 32 * s + 4 * g + q4;
                 const int r1 = r0 + 16;
-                const h16x4 va = ds_read_tr(&Vl[r0 * HD + swz(r0, ch) * 8 + within]);
-                const h16x4 vb = ds_read_tr(&Vl[r1 * HD + swz(r1, ch) * 8 + within]);
+                const h16x4 va = ds_read_tr(&Vl[r0 * HD + swzv(r0, ch) * 8 + within]);
+                const h16x4 vb = ds_read_tr(&Vl[r1 * HD + swzv(r1, ch) * 8 + within]);
                 h16x8 vf;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {

@@ -50,15 +50,41 @@ __device__ __forceinline__ int heads_window(const GemmArgs& g, int b) { return g
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
+// m / d for 0 <= m, 1 <= d.  Below 2^22 by a float reciprocal and one correction step
+// (the estimate q·(1 ± 2^-22) is within 1 of the quotient there): ≈ 8 VALU instead of the
+// ≈ 30 of an integer division (64-bit: more), which the tile epilogues did per output piece
+// for the grouped-row and head-major addresses (90 division sequences in the fp32-residual
+// kernel's ISA).  Exact either way.
+__device__ __forceinline__ int fast_div(int m, int d) {
+    if (m >= (1 << 22)) return m / d;
+    int q = (int)((float)m * __builtin_amdgcn_rcpf((float)d));
+    const int r = m - q * d;
+    q += (r >= d ? 1 : 0) - (r < 0 ? 1 : 0);
+    return q;
+}
+
+// element offset of output row m in the grouped layout (c_grp_rows rows per group,
+// c_grp_stride elements between groups); one group: no division (a uniform branch)
+__device__ __forceinline__ int64_t c_row(const GemmArgs& g, int m) {
+    if (g.c_grp_rows >= g.M) return (int64_t)m * g.ldc;
+    const int q = fast_div(m, g.c_grp_rows);
+    return (int64_t)q * g.c_grp_stride + (int64_t)(m - q * g.c_grp_rows) * g.ldc;
+}
+// m's row within its group (the positional table's row for EPI_F32_GELU_POS)
+__device__ __forceinline__ int c_rin(const GemmArgs& g, int m) {
+    return g.c_grp_rows >= g.M ? m : m - fast_div(m, g.c_grp_rows) * g.c_grp_rows;
+}
+
 __device__ __forceinline__ const h16* grp_row(const h16* base, int64_t m, int64_t grp_rows, int64_t grp_stride,
                                               int64_t ld) {
-    return base + (m / grp_rows) * grp_stride + (m % grp_rows) * ld;
+    const int q = fast_div((int)m, (int)grp_rows);
+    return base + (int64_t)q * grp_stride + (m - (int64_t)q * grp_rows) * ld;
 }
 
 template <int EPI>
 __device__ __forceinline__ void store_one(const GemmArgs& g, int m, int n, float v) {
     if (g.bias) v += g.bias[n];
-    const int64_t grp = m / g.c_grp_rows, r = m % g.c_grp_rows;
+    const int64_t grp = fast_div(m, g.c_grp_rows), r = m - grp * g.c_grp_rows;
     if constexpr (EPI == EPI_F16 || EPI == EPI_F16_GELU) {
         if (EPI == EPI_F16_GELU) v = gelu_erf(v);
         h16* C = (h16*)g.C + grp * g.c_grp_stride + r * g.ldc;
@@ -74,8 +100,9 @@ __device__ __forceinline__ void store_one(const GemmArgs& g, int m, int n, float
         C[n] = v;
     } else {  // EPI_HEADS: n = which*D + h*64 + d ; m = b*T + t
         const int D = g.heads_H * 64;
-        const int which = n / D, h = (n % D) >> 6, d = n & 63;
-        const int b = heads_window(g, m / g.heads_T), t = m % g.heads_T;
+        const int which = fast_div(n, D), h = (n - which * D) >> 6, d = n & 63;
+        const int bq = fast_div(m, g.heads_T);
+                const int b = heads_window(g, bq), t = m - bq * g.heads_T;
         h16* C = (h16*)g.C;
         C[((((int64_t)which * g.heads_nb + b) * g.heads_H + h) * g.heads_T + t) * 64 + d] = (h16)v;
     }
@@ -137,11 +164,12 @@ __device__ __forceinline__ void staged_epilogue_sq(const GemmArgs& g, const f32x
             h16* dst;
             if constexpr (EPI == EPI_HEADS) {
                 const int D = g.heads_H * 64;
-                const int which = n / D, h = (n % D) >> 6, d = n & 63;
-                const int b = heads_window(g, m / g.heads_T), t = m % g.heads_T;
+                const int which = fast_div(n, D), h = (n - which * D) >> 6, d = n & 63;
+                const int bq = fast_div(m, g.heads_T);
+                const int b = heads_window(g, bq), t = m - bq * g.heads_T;
                 dst = (h16*)g.C + ((((int64_t)which * g.heads_nb + b) * g.heads_H + h) * g.heads_T + t) * 64 + d;
             } else {
-                dst = (h16*)g.C + (m / g.c_grp_rows) * g.c_grp_stride + (int64_t)(m % g.c_grp_rows) * g.ldc + n;
+                dst = (h16*)g.C + c_row(g, m) + n;
             }
             *(h16x8*)dst = val;
         }
@@ -168,9 +196,8 @@ __device__ __forceinline__ void staged_epilogue_sq(const GemmArgs& g, const f32x
             const int row = id / (TM / 4), c4 = (id % (TM / 4)) * 4;
             const int m = min(m0 + row, g.M - 1), n = min(n0 + c4, g.N - 4);
             if constexpr (EPI == EPI_F32_RESID)
-                aux[j] = *(const f32x4*)((float*)g.C + (m / g.c_grp_rows) * g.c_grp_stride +
-                                         (int64_t)(m % g.c_grp_rows) * g.ldc + n);
-            if constexpr (EPI == EPI_F32_GELU_POS) aux[j] = *(const f32x4*)&g.pos[(int64_t)(m % g.c_grp_rows) * g.N + n];
+                aux[j] = *(const f32x4*)((float*)g.C + c_row(g, m) + n);
+            if constexpr (EPI == EPI_F32_GELU_POS) aux[j] = *(const f32x4*)&g.pos[(int64_t)c_rin(g, m) * g.N + n];
         }
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
@@ -179,7 +206,7 @@ __device__ __forceinline__ void staged_epilogue_sq(const GemmArgs& g, const f32x
             const int m = m0 + row, n = n0 + c4;
             if (m >= g.M || n >= g.N) continue;
             f32x4 val = *(const f32x4*)&T[at(row, c4)];
-            float* dst = (float*)g.C + (m / g.c_grp_rows) * g.c_grp_stride + (int64_t)(m % g.c_grp_rows) * g.ldc + n;
+            float* dst = (float*)g.C + c_row(g, m) + n;
             if constexpr (EPI == EPI_F32_RESID) val += aux[j];
             if constexpr (EPI == EPI_F32_GELU_POS) {
 #pragma unroll
@@ -301,7 +328,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g) {
                 if (n >= g.N) continue;
                 if constexpr (EPI == EPI_F32) {  // decoder logits: written through L2 for the select kernels
                     const float v = g.bias ? acc[mi][ni][i] + g.bias[n] : acc[mi][ni][i];
-                    const int64_t grp = m / g.c_grp_rows, r = m % g.c_grp_rows;
+                    const int64_t grp = fast_div(m, g.c_grp_rows), r = m - grp * g.c_grp_rows;
                     __hip_atomic_store((float*)g.C + grp * g.c_grp_stride + r * g.ldc + n, v, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                 } else
@@ -414,11 +441,12 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
             h16* dst;
             if constexpr (EPI == EPI_HEADS) {
                 const int D = g.heads_H * 64;
-                const int which = n / D, h = (n % D) >> 6, d = n & 63;
-                const int b = heads_window(g, m / g.heads_T), t = m % g.heads_T;
+                const int which = fast_div(n, D), h = (n - which * D) >> 6, d = n & 63;
+                const int bq = fast_div(m, g.heads_T);
+                const int b = heads_window(g, bq), t = m - bq * g.heads_T;
                 dst = (h16*)g.C + ((((int64_t)which * g.heads_nb + b) * g.heads_H + h) * g.heads_T + t) * 64 + d;
             } else {
-                dst = (h16*)g.C + (m / g.c_grp_rows) * g.c_grp_stride + (int64_t)(m % g.c_grp_rows) * g.ldc + n;
+                dst = (h16*)g.C + c_row(g, m) + n;
             }
             __builtin_nontemporal_store(v, (h16x8*)dst);
         }
@@ -457,10 +485,9 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
                 const int row = id >> 6, c4 = (id & 63) * 4;
                 const int m = min(m0 + half * 128 + row, g.M - 1), n = min(n0 + c4, g.N - 4);
                 if constexpr (EPI == EPI_F32_RESID)
-                    aux[jj] = *(const f32x4*)((float*)g.C + (m / g.c_grp_rows) * g.c_grp_stride +
-                                              (int64_t)(m % g.c_grp_rows) * g.ldc + n);
+                    aux[jj] = *(const f32x4*)((float*)g.C + c_row(g, m) + n);
                 if constexpr (EPI == EPI_F32_GELU_POS)
-                    aux[jj] = *(const f32x4*)&g.pos[(int64_t)(m % g.c_grp_rows) * g.N + n];
+                    aux[jj] = *(const f32x4*)&g.pos[(int64_t)c_rin(g, m) * g.N + n];
             }
 #pragma unroll
             for (int jj = 0; jj < AB; ++jj) {
@@ -470,8 +497,7 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
                 const int m = m0 + half * 128 + row, n = n0 + c4;
                 if (m < g.M && n < g.N) {
                     f32x4 v = *(const f32x4*)&T[ep32(row, c4)] + b4;
-                    float* dst = (float*)g.C + (m / g.c_grp_rows) * g.c_grp_stride +
-                                 (int64_t)(m % g.c_grp_rows) * g.ldc + n;
+                    float* dst = (float*)g.C + c_row(g, m) + n;
                     if constexpr (EPI == EPI_F32_RESID) v += aux[jj];
                     if constexpr (EPI == EPI_F32_GELU_POS) {
 #pragma unroll
@@ -701,11 +727,12 @@ __device__ __forceinline__ void staged_epilogue_next0(const GemmArgs& g, f32x4 (
                 h16* dst;
                 if constexpr (EPI == EPI_HEADS) {
                     const int D = g.heads_H * 64;
-                    const int which = n / D, h = (n % D) >> 6, d = n & 63;
-                    const int b = heads_window(g, m / g.heads_T), t = m % g.heads_T;
+                    const int which = fast_div(n, D), h = (n - which * D) >> 6, d = n & 63;
+                    const int bq = fast_div(m, g.heads_T);
+                const int b = heads_window(g, bq), t = m - bq * g.heads_T;
                     dst = (h16*)g.C + ((((int64_t)which * g.heads_nb + b) * g.heads_H + h) * g.heads_T + t) * 64 + d;
                 } else {
-                    dst = (h16*)g.C + (m / g.c_grp_rows) * g.c_grp_stride + (int64_t)(m % g.c_grp_rows) * g.ldc + n;
+                    dst = (h16*)g.C + c_row(g, m) + n;
                 }
                 __builtin_nontemporal_store(v, (h16x8*)dst);
             }
@@ -739,10 +766,9 @@ __device__ __forceinline__ void staged_epilogue_next0(const GemmArgs& g, f32x4 (
                     const int row = id >> 6, c4 = (id & 63) * 4;
                     const int m = min(m0 + pass * PR + row, g.M - 1), n = min(n0 + c4, g.N - 4);
                     if constexpr (EPI == EPI_F32_RESID)
-                        aux[jj] = *(const f32x4*)((float*)g.C + (m / g.c_grp_rows) * g.c_grp_stride +
-                                                  (int64_t)(m % g.c_grp_rows) * g.ldc + n);
+                        aux[jj] = *(const f32x4*)((float*)g.C + c_row(g, m) + n);
                     if constexpr (EPI == EPI_F32_GELU_POS)
-                        aux[jj] = *(const f32x4*)&g.pos[(int64_t)(m % g.c_grp_rows) * g.N + n];
+                        aux[jj] = *(const f32x4*)&g.pos[(int64_t)c_rin(g, m) * g.N + n];
                 }
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) {
@@ -751,7 +777,7 @@ __device__ __forceinline__ void staged_epilogue_next0(const GemmArgs& g, f32x4 (
                     const int m = m0 + pass * PR + row, n = n0 + c4;
                     if (m < g.M && n < g.N) {
                         f32x4 v = *(const f32x4*)&T[ep32(row, c4)] + b4;
-                        float* dst = (float*)g.C + (m / g.c_grp_rows) * g.c_grp_stride + (int64_t)(m % g.c_grp_rows) * g.ldc + n;
+                        float* dst = (float*)g.C + c_row(g, m) + n;
                         if constexpr (EPI == EPI_F32_RESID) v += aux[jj];
                         if constexpr (EPI == EPI_F32_GELU_POS) {
 #pragma unroll
@@ -1182,7 +1208,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm128_ring_kernel(GemmArgs g) {
 #pragma unroll
                 for (int ni = 0; ni < FT; ++ni) {
                     const int n = n0 + wn * WT + ni * 16 + (lane & 15);
-                    if (n < g.N) ((float*)g.C)[(m / g.c_grp_rows) * g.c_grp_stride + (int64_t)(m % g.c_grp_rows) * g.ldc + n] =
+                    if (n < g.N) ((float*)g.C)[c_row(g, m) + n] =
                         g.bias ? acc[mi][ni][i] + g.bias[n] : acc[mi][ni][i];
                 }
             }
@@ -1296,7 +1322,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm64_ring_kernel(GemmArgs g) {
                 if (n >= g.N) continue;
                 if constexpr (EPI == EPI_F32) {
                     const float v = g.bias ? acc[mi][ni][i] + g.bias[n] : acc[mi][ni][i];
-                    const int64_t grp = m / g.c_grp_rows, r = m % g.c_grp_rows;
+                    const int64_t grp = fast_div(m, g.c_grp_rows), r = m - grp * g.c_grp_rows;
                     __hip_atomic_store((float*)g.C + grp * g.c_grp_stride + r * g.ldc + n, v, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                 } else

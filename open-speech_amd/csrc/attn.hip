@@ -158,18 +158,12 @@ __device__ __forceinline__ void enc_attn_unit(const h16* __restrict__ qkv, h16* 
             const float mcs = -mnew * cs;
             float ls = 0.f;
             float p[4][4];
-            // the scale + shift of two scores per packed FMA (v_pk_fma_f32: the same fused
-            // multiply-add per element as fmaf, half the issue slots in this VALU-bound loop)
-            const f32x2 cs2 = {cs, cs}, mcs2 = {mcs, mcs};
 #pragma unroll
             for (int t = 0; t < 4; ++t)
 #pragma unroll
-                for (int i = 0; i < 4; i += 2) {
-                    const f32x2 x = __builtin_elementwise_fma(f32x2{sc[qt][t][i], sc[qt][t][i + 1]}, cs2, mcs2);
-                    p[t][i] = __builtin_amdgcn_exp2f(x.x);
+                for (int i = 0; i < 4; ++i) {
+                    p[t][i] = __builtin_amdgcn_exp2f(fmaf(sc[qt][t][i], cs, mcs));
                     ls += p[t][i];
-                    p[t][i + 1] = __builtin_amdgcn_exp2f(x.y);
-                    ls += p[t][i + 1];
                 }
             lrun[qt] = lrun[qt] * alpha + ls;
             if (rescale) {

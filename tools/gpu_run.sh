@@ -13,6 +13,7 @@
 #   b1          batch-1 greedy step breakdown               -> $O/b1_breakdown.txt
 #   b1beam      batch-1 beam-5 step breakdown               -> $O/b1beam_breakdown.txt
 #   pmcb1beam   SQ counter passes over a batch-1 beam-5 call -> $O/pmc_b1beam_{1,2}.txt
+#   pmcfetch:SCRIPT,ARGS  FETCH_SIZE per dispatch of $PMC_MATCH kernels over python3 SCRIPT ARGS -> $O/pmcfetch_N.txt
 #   pmcenc      the same SQ passes over one 64-window greedy step -> $O/pmc_enc_{1,2}.txt
 #   repro       tools/graph_prof_repro (mode 2) under a rocprofv3 kernel trace -> $O/repro.log
 #   bench:ARGS  bench.py with extra args (commas -> spaces) -> $O/bench_N.json
@@ -71,6 +72,14 @@ for s in "$@"; do
       rc=$?; [ $rc -eq 0 ] && python3 tools/b1_breakdown.py $O/b1bprof/run_kernel_trace.csv $((5*445)) > $O/b1beam_breakdown.txt && head -40 $O/b1beam_breakdown.txt
       [ $rc -eq 0 ] && python3 tools/step_timeline.py $O/b1bprof/run_kernel_trace.csv beam_update 1500 > $O/b1beam_step_timeline.txt && cat $O/b1beam_step_timeline.txt
       rm -f $O/b1bprof/run_kernel_trace.csv ;;
+    pmcfetch:*)
+      # FETCH_SIZE per dispatch of the kernels matching $PMC_MATCH (default gemm8p) over one script
+      A=${s#pmcfetch:}; A=${A//,/ }
+      timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pf_$i -o run -- python3 -u $A > $O/pf_$i.log 2>&1; rc=$?
+      CSV=$(find $O/pf_$i -name '*counter_collection.csv' | head -1)
+      [ -n "$CSV" ] && python3 tools/pmc_dispatch.py $CSV FETCH_SIZE ${PMC_MATCH:-gemm8p} > $O/pmcfetch_$i.txt
+      find $O/pf_$i -name '*.csv' -delete
+      [ $rc -eq 0 ] && head -40 $O/pmcfetch_$i.txt ;;
     pmcenc)
       # the same SQ counter passes over one 64-window greedy step (one lane)
       for f in 1 2; do

@@ -1065,15 +1065,17 @@ void launch8p(const GemmArgs& g0, hipStream_t s) {
     set_lds_once((const void*)gemm8p_kernel<EPI, DBG>, lds);
     GemmArgs g = g0;
     g.band = choose_band(g);
-    // the next tile's first K-tile staged during the epilogue: only the head-major qkv
-    // epilogue gains (1054 -> 1027 us per launch at 64 windows); the fp32 epilogues in four
-    // 64-row passes (o, fc2: 886 -> 956 us) and the GELU one (1485 -> 1535 us) lose, measured.
-    // OSW_GEMM_NEXT0=0: never, =1: every epilogue.
+    // the next tile's first K-tile staged during the epilogue.  Round 3: only the head-major
+    // qkv epilogue gained (1054 -> 1027 us per launch at 64 windows); the fp32 epilogues in
+    // four 64-row passes (o, fc2: 886 -> 956 us) and the GELU one (1485 -> 1535 us) lost.
+    // Round 6, after the epilogue work: the GELU one gains (1301 -> 1289 us), the head-major
+    // one no longer does (930 without vs 940 with), the fp32 ones still lose (751 -> 779 us)
+    // (profiles/r06_z_next0_ab.txt).  OSW_GEMM_NEXT0=0: never, =1: every epilogue.
     static const int next0_env = [] {
         const char* e = std::getenv("OSW_GEMM_NEXT0");
         return e ? (e[0] == '1' ? 1 : 0) : -1;
     }();
-    const bool next0 = next0_env < 0 ? EPI == EPI_HEADS : next0_env == 1;
+    const bool next0 = next0_env < 0 ? EPI == EPI_F16_GELU : next0_env == 1;
     g.kc = next0 ? 1 : 0;  // (kc is unused by the 8-phase kernel otherwise)
     const int nwg = ((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
     static const int cus = [] {

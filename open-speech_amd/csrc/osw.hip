@@ -1908,10 +1908,12 @@ int session_step(osw_ctx* c, int max_chunks, int refill_min, osw_window_result* 
     REQUIRE(r && r->tokens && r->n_tokens && r->sum_logprob && r->no_speech_prob && r->language && tags,
             "null result argument");
     REQUIRE(cap >= S->W, "cap must hold every slot (max_batch)");
-    // OSW_SESSION_CHUNK: decoder steps between admission points (default 8, as decode())
+    // OSW_SESSION_CHUNK: decoder steps between admission points.  4 since round 6 (config 5
+    // 177-179 vs 171-172 calls/s, REST mixed continuous 74-75 vs 73 calls/s with p50 117-122
+    // vs 136-141 ms: profiles/r06_zcd_session_chunk_ab.txt); 8 before (decode()'s chunk)
     static const int CH = [] {
         const char* e = getenv("OSW_SESSION_CHUNK");
-        return e ? std::max(1, std::min(64, atoi(e))) : 8;
+        return e ? std::max(1, std::min(64, atoi(e))) : 4;
     }();
     const int beam = S->beam;
     int done = 0;

@@ -24,7 +24,7 @@ batches are ``max_batch`` anyway.
 Continuous batching (``continuous``, the backend's default): every lane drives a decode
 session instead (``_SessionLane``, osw_session_*): a request's windows are queued into
 the session one at a time as its seek loop advances, free decoder slots are refilled
-between chunks of 8 decoder steps, so a request arriving mid-batch starts within a chunk
+between chunks of 4 decoder steps (OSW_SESSION_CHUNK), so a request arriving mid-batch starts within a chunk
 and a batch costs what its windows' own lengths cost.  Lanes take turns on the encoder
 the same way (a session's admission is an encoder call counted on the GPU's queue).
 
@@ -201,7 +201,7 @@ class _SessionLane(_Worker):
     lane's session when the request is taken, and each finished window is consumed
     (segments.consume_window) and the clip's next window queued at once, so windows of
     different requests and different seek positions decode side by side and a finished
-    window's slot is refilled between chunks of 8 decoder steps instead of waiting for
+    window's slot is refilled between chunks of 4 decoder steps instead of waiting for
     the batch's longest window.  A session holds one decode configuration
     (``TranscribeOptions.key()``): a lane admits only requests of its session's key, and
     opens a session for another key once its own has drained.  Requests a session cannot

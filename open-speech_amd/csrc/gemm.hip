@@ -376,9 +376,15 @@ __device__ __forceinline__ int acc_col(int wn, int ni) { return IL ? (ni >> 1) *
 // the MFMA operands), lane l of block (mi, ni) holding C[row + (l & 15)][col + 4 (l >> 4) + e],
 // so the image takes one 8-B write per block instead of four 2-B ones
 // (fc1 at 64 windows 1488 -> 1432 us, + GELU 1694 -> 1627 us; profiles/r04_s_epilogue.jsonl, r04_t_epilogue_forms.jsonl)
-template <int EPI, bool IL = false, bool TR = false>
+// TN: the tile's width (256; 128 for the half-width tile, whose waves hold accumulator
+// blocks ni < 2 only): the image keeps its 256-wide rows, the copy-out covers TN columns
+template <int EPI, bool IL = false, bool TR = false, int TN = 256>
 __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], int m0, int n0, int wm,
                                                 int wn, char* smem, int tid) {
+    static_assert(TN == 256 || (TN == 128 && IL), "the half-width tile is the 8-phase layout");
+    constexpr int NI = TN / 64;        // accumulator column blocks per wave
+    constexpr int C16 = TN / 8;        // 16-B fp16 chunks per image row
+    constexpr int C32 = TN / 4;        // 16-B fp32 chunks per image row
     const int lane = tid & 63;
     // the bias of this thread's columns, loaded once per tile (epi_apply): TR, 4 columns per
     // accumulator block (one 16-B load each); otherwise one column per block
@@ -388,7 +394,7 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
     f32x4 bt[4];
     float bs[4];
 #pragma unroll
-    for (int ni = 0; ni < 4 && F16; ++ni) {
+    for (int ni = 0; ni < NI && F16; ++ni) {
         if constexpr (TR) {
             const int n = min(n0 + acc_col<IL>(wn, ni) + 4 * (lane >> 4), g.N - 4);
             bt[ni] = hb ? *(const f32x4*)(g.bias + n) : f32x4{-0.f, -0.f, -0.f, -0.f};
@@ -409,7 +415,7 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
 #pragma unroll
             for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
-                for (int ni = 0; ni < 4; ++ni) {
+                for (int ni = 0; ni < NI; ++ni) {
                     if (IL && (mi >> 2) != half) continue;
                     const int row = acc_row<IL>(wm, mi) + (lane & 15);
                     const int col = acc_col<IL>(wn, ni) + 4 * (lane >> 4);
@@ -422,7 +428,7 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
 #pragma unroll
         for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni)
+            for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     if (IL && (mi >> 2) != half) continue;
@@ -432,9 +438,9 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
                 }
         __syncthreads();
 #pragma unroll 4
-        for (int j = 0; j < 16 / NH; ++j) {
+        for (int j = 0; j < 256 * C16 / GNT / NH; ++j) {
             const int id = j * GNT + tid;
-            const int row = half * 128 + (id >> 5), c8 = (id & 31) * 8;
+            const int row = half * 128 + id / C16, c8 = (id % C16) * 8;
             const int m = m0 + row, n = n0 + c8;
             if (m >= g.M || n >= g.N) continue;
             const h16x8 v = *(const h16x8*)&T[ep16(row, c8)];
@@ -454,14 +460,14 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
     } else {
         float* T = (float*)smem;
         // this thread's 4 copy-out columns are the same in every piece (GNT % 64 == 0)
-        const f32x4 b4 = hb ? *(const f32x4*)(g.bias + min(n0 + (tid & 63) * 4, g.N - 4))
+        const f32x4 b4 = hb ? *(const f32x4*)(g.bias + min(n0 + (tid % C32) * 4, g.N - 4))
                             : f32x4{-0.f, -0.f, -0.f, -0.f};
         for (int half = 0; half < 2; ++half) {
             if (IL || wm == half) {
 #pragma unroll
                 for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
-                    for (int ni = 0; ni < 4; ++ni)
+                    for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
                         for (int i = 0; i < 4; ++i) {
                             if (IL && (mi >> 2) != half) continue;
@@ -476,13 +482,14 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
             // vmcnt(0) wait, which also waited for the previous piece's store).  AB = 8 when
             // only the other half's accumulators are live (IL); 1 when all are (more spilled).
             constexpr int AB = IL ? 8 : 1;
+            constexpr int NJ = 128 * C32 / GNT;  // pieces per thread per half
 #pragma unroll
-            for (int j0 = 0; j0 < 16; j0 += AB) {
+            for (int j0 = 0; j0 < NJ; j0 += AB) {
             f32x4 aux[EPI == EPI_F32_RESID || EPI == EPI_F32_GELU_POS ? AB : 1];
 #pragma unroll
             for (int jj = 0; jj < AB; ++jj) {
                 const int id = (j0 + jj) * GNT + tid;
-                const int row = id >> 6, c4 = (id & 63) * 4;
+                const int row = id / C32, c4 = (id % C32) * 4;
                 const int m = min(m0 + half * 128 + row, g.M - 1), n = min(n0 + c4, g.N - 4);
                 if constexpr (EPI == EPI_F32_RESID)
                     aux[jj] = *(const f32x4*)((float*)g.C + c_row(g, m) + n);
@@ -493,7 +500,7 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
             for (int jj = 0; jj < AB; ++jj) {
                 const int j = j0 + jj;
                 const int id = j * GNT + tid;
-                const int row = id >> 6, c4 = (id & 63) * 4;
+                const int row = id / C32, c4 = (id % C32) * 4;
                 const int m = m0 + half * 128 + row, n = n0 + c4;
                 if (m < g.M && n < g.N) {
                     f32x4 v = *(const f32x4*)&T[ep32(row, c4)] + b4;
@@ -591,9 +598,9 @@ __global__ __launch_bounds__(GNT, 1) void gemm256_kernel(GemmArgs g) {
 
 // band width minimising modelled L2-miss bytes: A re-read once per band, a band's
 // weights re-read once per 32/G concurrently resident row panels of an XCD
-int choose_band(const GemmArgs& g) {
+int choose_band(const GemmArgs& g, int tn = GB) {
     if (const char* e = getenv("OSW_GEMM_BAND")) return atoi(e);
-    const int ntn = (g.N + GB - 1) / GB, ntm = (g.M + GB - 1) / GB;
+    const int ntn = (g.N + tn - 1) / tn, ntm = (g.M + GB - 1) / GB;
     const double abytes = (double)g.M * g.K * 2, wbytes = (double)g.N * g.K * 2;
     int best = ntn;
     double bc = 1e300;
@@ -634,15 +641,17 @@ void launch256(const GemmArgs& g0, hipStream_t s) {
 constexpr int HT = 128 * BK;  // halfs per half-tile
 
 // tile origin of virtual workgroup id `bid` (XCD-contiguous runs, column bands of G tiles)
+// (TN: the tile's width, 256 or 128 for the half-width tile gemm8h_kernel)
+template <int TN = GB>
 __device__ __forceinline__ void tile8p_origin(const GemmArgs& g, int bid, int& m0, int& n0) {
-    const int ntn = (g.N + GB - 1) / GB, ntm = (g.M + GB - 1) / GB;
+    const int ntn = (g.N + TN - 1) / TN, ntm = (g.M + GB - 1) / GB;
     const int nwg = ntn * ntm;
     const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
     const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
     const int G = g.band > 0 ? min(g.band, ntn) : ntn;
     const int band = tile / (G * ntm), rr0 = tile % (G * ntm);
     const int gw = min(G, ntn - band * G);
-    n0 = (band * G + rr0 % gw) * GB;
+    n0 = (band * G + rr0 % gw) * TN;
     m0 = (rr0 / gw) * GB;
 }
 
@@ -1099,6 +1108,193 @@ void launch8p(const GemmArgs& g0, hipStream_t s) {
     }();
     const int grid_cap = per_tile ? 1 << 30 : g.share_cus ? shared_cap : cus;
     gemm8p_kernel<EPI, DBG><<<std::min(nwg, std::max(8, grid_cap)), GNT, lds, s>>>(g);
+}
+
+// Half-width tile (256 x 128 x 64) for the encoder at one to a few windows, where the 256²
+// tile leaves CUs idle (qkv at one window: 90 tiles on 256 CUs) or runs a second, mostly
+// empty round (fc2 at four windows: 120 tiles of 4x the K).  Same 8 waves in two groups one
+// barrier apart and the same per-wave accumulator layout as gemm8p_tile restricted to the
+// W0 half (rows {0,128} + wm*64 + [0,64), cols wn*32 + [0,32)), so every output element is
+// the same MFMA chain over K in the same order as in the other tiles: identical results.
+// Two phases per K-tile — 1: quadrant (0,0) from A0 + W0, 2: quadrant (1,0) from A1 with
+// W0's fragments kept in registers — and a 3-slot ring of {A0, A1, W0} (144 KiB) so a
+// K-tile is staged two tiles ahead: phase 1 of tile t stages A0(t+2), W0(t+2) (their slots'
+// last reads were phase 1 of t-1, two phases back), phase 2 stages A1(t+2) and retires
+// tile t+1 (vmcnt(6): tile t+2's three half-tiles stay in flight).  Persistent like
+// gemm8p_kernel (one workgroup per CU looping over tiles).
+constexpr int H8_SLOTS = 3, H8_LDS = H8_SLOTS * 3 * HT * 2;  // 147456 B
+static_assert(H8_LDS >= EPI_LDS, "the epilogue image fits the ring");
+
+template <int EPI, int DBG>
+__device__ __forceinline__ void gemm8h_tile(const GemmArgs& g, int bid, h16* smem, int tid) {
+    const int wave = tid >> 6, lane = tid & 63;
+    constexpr bool TR = EPI == EPI_F16 || EPI == EPI_F16_GELU;
+    int m0, n0;
+    tile8p_origin<128>(g, bid, m0, n0);
+    const h16* src[3][2];  // half-tiles 0: A0, 1: A1, 2: W0 (src8p's numbering)
+#pragma unroll
+    for (int H = 0; H < 3; ++H)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) src[H][i] = src8p(g, m0, n0, H, i, wave, lane);
+    auto stage = [&](int H, int t) {
+        h16* base = smem + ((t % H8_SLOTS) * 3 + H) * HT;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(src[H][i] + t * BK),
+                                             (OSW_LDS void*)(base + (i * 8 + wave) * 8 * BK), 16, 0, 0);
+    };
+    const int wm = wave >> 2, wn = wave & 3;
+    const int li = lane & 15, lc = lane >> 4;
+    const int aoff0 = (wm * 64 + li) * BK + swz(wm * 64 + li, lc) * 8;
+    const int aoff1 = (wm * 64 + li) * BK + swz(wm * 64 + li, 4 + lc) * 8;
+    const int boff0 = (wn * 32 + li) * BK + swz(wn * 32 + li, lc) * 8;
+    const int boff1 = (wn * 32 + li) * BK + swz(wn * 32 + li, 4 + lc) * 8;
+    f32x4 acc[8][4];  // blocks ni < 2 only (the epilogue's TN = 128 form reads no others)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    h16x8 af[4][2], bf[2][2];
+    auto read_a = [&](const h16* hb) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+            af[mt][0] = *(const h16x8*)&hb[aoff0 + mt * 16 * BK];
+            af[mt][1] = *(const h16x8*)&hb[aoff1 + mt * 16 * BK];
+        }
+    };
+    auto read_b = [&](const h16* hb) {
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+            bf[nt][0] = *(const h16x8*)&hb[boff0 + nt * 16 * BK];
+            bf[nt][1] = *(const h16x8*)&hb[boff1 + nt * 16 * BK];
+        }
+    };
+    auto barrier = [] {
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+    auto mfma = [&](int a) {  // quadrant (a, 0), the 8-phase kernel's MFMA order
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                f32x4 c = acc[a * 4 + mt][nt];
+                if constexpr (TR) {
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[nt][0], af[mt][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[nt][1], af[mt][1], c, 0, 0, 0);
+                } else {
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mt][0], bf[nt][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mt][1], bf[nt][1], c, 0, 0, 0);
+                }
+                acc[a * 4 + mt][nt] = c;
+            }
+        __builtin_amdgcn_s_setprio(0);
+    };
+    const int nk = g.K / BK;
+    // prologue: tiles 0 and 1 (issue order A0 W0 A1), tile 0 retired
+    stage(0, 0);
+    stage(2, 0);
+    stage(1, 0);
+    if (nk > 1) {
+        stage(0, 1);
+        stage(2, 1);
+        stage(1, 1);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    barrier();
+    if (__builtin_amdgcn_readfirstlane(wave) >= 4) barrier();  // group 1 runs one barrier behind group 0
+    for (int t = 0; t < nk; ++t) {
+        const h16* buf = smem + (t % H8_SLOTS) * 3 * HT;
+        const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
+        // phase 1: quadrant (0,0) from A0, W0
+        if (n2) {
+            stage(0, t + 2);
+            stage(2, t + 2);
+        }
+        read_a(buf + 0 * HT);
+        read_b(buf + 2 * HT);
+        barrier();
+        mfma(0);
+        barrier();
+        // phase 2: quadrant (1,0) from A1 (W0's fragments still in registers); retire tile t+1
+        if (n2) {
+            stage(1, t + 2);
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else if (n1) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        read_a(buf + 1 * HT);
+        barrier();
+        mfma(1);
+        barrier();
+    }
+    if (__builtin_amdgcn_readfirstlane(wave) < 4) barrier();
+    if constexpr (DBG == 1) {
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+        if (t == 1234.5f) ((float*)g.C)[tid] = t;  // keeps the loop live
+    } else {
+        staged_epilogue<EPI, true, TR, 128>(g, acc, m0, n0, wm, wn, (char*)smem, tid);
+    }
+}
+
+template <int EPI, int DBG = 0>
+__global__ __launch_bounds__(GNT, 1) void gemm8h_kernel(GemmArgs g) {
+    extern __shared__ __attribute__((aligned(16))) h16 smem[];  // [3][A0 A1 W0][128*64]
+    const int nwg = ((g.N + 127) / 128) * ((g.M + GB - 1) / GB);
+    for (int vb = blockIdx.x; vb < nwg; vb += gridDim.x) {
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));  // nothing derived from it is kept live across tiles
+        gemm8h_tile<EPI, DBG>(g, vb, smem, tid);
+        __syncthreads();  // the epilogue's LDS image is the next tile's operand ring
+    }
+}
+
+// The GEMM's persistent grid: every CU, or 3/4 of them while sibling lanes have calls in
+// flight (launch8p's rule)
+int grid8(const GemmArgs& g) {
+    static const int cus = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return 256;
+        return n;
+    }();
+    return g.share_cus ? std::max(8, cus * 3 / 4 / 8 * 8) : cus;
+}
+
+// The half-width tile for few-window encoder GEMMs (profiles/r06_s2b_small_gemm.jsonl: every
+// tile variant on the five encoder shapes at 1-4 windows).  A half tile costs about half a
+// 256² tile, so with G workgroups the two grids take ceil(T/G) and ½·ceil(2T/G) tile rounds:
+// the half tile where that is fewer (one window: qkv, fc1 fill one round instead of a third
+// of the CUs; three and four windows: a 1.05-1.4-round 256² grid becomes 1.5 rounds' worth),
+// from 90 256² tiles (below that the 64 / 128 tiles' 2-8x the workgroups win: the
+// out-projection and fc2 at one or two windows) up to 512 (the 64-window batches keep the
+// tuned 8-phase grid and its 32 KiB of LDS left for other lanes' decoders: the half tile's
+// 3-slot ring takes 144 KiB).  OSW_GEMM_HALF=0 turns it off (A/B switch).
+bool use_half_tile(const GemmArgs& g, int64_t t8) {
+    static const bool on = [] {
+        const char* e = std::getenv("OSW_GEMM_HALF");
+        return !(e && e[0] == '0');
+    }();
+    if (!on || g.A_lo || g.kc != 0 || g.N % 8 != 0 || t8 < 90 || t8 >= 512) return false;
+    const int64_t G = grid8(g), th = (int64_t)((g.N + 127) / 128) * ((g.M + GB - 1) / GB);
+    return ((th + G - 1) / G) < 2 * ((t8 + G - 1) / G);
+}
+
+template <int EPI, int DBG = 0>
+void launch8h(const GemmArgs& g0, hipStream_t s) {
+    set_lds_once((const void*)gemm8h_kernel<EPI, DBG>, H8_LDS);
+    GemmArgs g = g0;
+    g.band = choose_band(g, 128);
+    const int nwg = ((g.N + 127) / 128) * ((g.M + GB - 1) / GB);
+    gemm8h_kernel<EPI, DBG><<<std::min(nwg, grid8(g)), GNT, H8_LDS, s>>>(g);
 }
 
 
@@ -2180,6 +2376,7 @@ void prepare_gemm_kernels() {
             set_lds_once((const void*)gemm256_kernel<E>, l256);
             set_lds_once((const void*)gemm8p_kernel<E, 0>, l8p);
             set_lds_once((const void*)gemm128_ring_kernel<E>, R128_LDS);
+            set_lds_once((const void*)gemm8h_kernel<E, 0>, H8_LDS);
         };
         each(std::integral_constant<int, EPI_F16>{});
         each(std::integral_constant<int, EPI_F16_GELU>{});
@@ -2188,6 +2385,7 @@ void prepare_gemm_kernels() {
         each(std::integral_constant<int, EPI_F32>{});
         each(std::integral_constant<int, EPI_HEADS>{});
         set_lds_once((const void*)gemm8p_kernel<EPI_F32, 1>, l8p);
+        set_lds_once((const void*)gemm8h_kernel<EPI_F32, 1>, H8_LDS);
         set_lds_once((const void*)gemm8p_kernel<EPI_F16, 2>, l8p);
         set_lds_once((const void*)gemm8p_kernel<EPI_F16_GELU, 2>, l8p);
         set_lds_once((const void*)gemm_wide_kernel<true, 256>, wide_lds<256>(true));
@@ -2219,6 +2417,16 @@ void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s) {
         return e ? atoi(e) : 180;
     }();
     const int64_t big_tiles = (int64_t)((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
+    if (variant == 0 && use_half_tile(g, big_tiles)) {
+        switch (g.epi) {
+            case EPI_F16: launch8h<EPI_F16>(g, s); return;
+            case EPI_F16_GELU: launch8h<EPI_F16_GELU>(g, s); return;
+            case EPI_F32_RESID: launch8h<EPI_F32_RESID>(g, s); return;
+            case EPI_F32_GELU_POS: launch8h<EPI_F32_GELU_POS>(g, s); return;
+            case EPI_F32: launch8h<EPI_F32>(g, s); return;
+            default: launch8h<EPI_HEADS>(g, s); return;
+        }
+    }
     const bool big = !g.A_lo && (variant == 2 || (variant == 0 && big_tiles >= p8_min && g.N % 8 == 0 &&
                                                    !getenv("OSW_GEMM128")));
 
@@ -2242,6 +2450,25 @@ void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s) {
     if (variant == 15) {
         launch8p<EPI_F16, 3>(g, s);
         return;
+    }
+    if (variant == 17) {  // debug: the half-width tile's main loop alone
+        launch8h<EPI_F32, 1>(g, s);
+        return;
+    }
+    if (variant == 18 || variant == 19) {  // debug: the half-width tile, fp16 / GELU fp16 out
+        if (variant == 18) launch8h<EPI_F16>(g, s);
+        else launch8h<EPI_F16_GELU>(g, s);
+        return;
+    }
+    if (variant == 16 && !g.A_lo && g.N % 8 == 0) {  // the half-width 256 x 128 tile
+        switch (g.epi) {
+            case EPI_F16: launch8h<EPI_F16>(g, s); return;
+            case EPI_F16_GELU: launch8h<EPI_F16_GELU>(g, s); return;
+            case EPI_F32_RESID: launch8h<EPI_F32_RESID>(g, s); return;
+            case EPI_F32_GELU_POS: launch8h<EPI_F32_GELU_POS>(g, s); return;
+            case EPI_F32: launch8h<EPI_F32>(g, s); return;
+            default: launch8h<EPI_HEADS>(g, s); return;
+        }
     }
     if (variant == 12 || variant == 13) {  // debug: fp16 / GELU epilogues on accumulators not transposed
         if (variant == 12) launch8p<EPI_F16, 2>(g, s);

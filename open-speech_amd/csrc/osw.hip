@@ -2392,7 +2392,7 @@ int osw_debug_gemm(osw_ctx* c, int32_t M, int32_t N, int32_t K, int32_t variant,
         REQUIRE(c && A && Wt && C && ms, "null argument");
         REQUIRE(M >= 1 && N >= 1 && K >= 64 && K % 64 == 0 && iters >= 1, "bad GEMM shape");
         REQUIRE(variant != 3 || (M <= 64 && K % 128 == 0), "skinny needs M <= 64 and K % 128 == 0");
-        REQUIRE(variant < 8 || variant > 13 || variant == 11 || N % 8 == 0,
+        REQUIRE(variant < 8 || variant > 19 || variant == 11 || N % 8 == 0,
                 "the 8-phase debug variants need N % 8 == 0 (their epilogues store 8-column chunks)");
         std::lock_guard<std::mutex> lk(c->mu);
         DeviceScope dev_scope_((c->device));

@@ -26,7 +26,9 @@ def eng():
     (5, 64, 51866, 1280), (5, 1, 51866, 1280), (5, 37, 20000, 384), (5, 64, 300, 64), (5, 5, 1000, 128),
     (6, 1500, 1280, 1280), (6, 300, 200, 128), (6, 1500, 5120, 1280), (6, 1500, 1280, 5120),
     (7, 1500, 1280, 1280), (7, 300, 200, 128), (11, 1500, 1280, 1280), (11, 300, 200, 128),
-    (11, 1500, 5120, 1280), (11, 1500, 1280, 5120), (11, 6000, 3840, 1280), (11, 2999, 776, 192)])
+    (11, 1500, 5120, 1280), (11, 1500, 1280, 5120), (11, 6000, 3840, 1280), (11, 2999, 776, 192),
+    (16, 1500, 3840, 1280), (16, 1500, 1280, 5120), (16, 700, 264, 128), (16, 513, 1000, 64), (16, 6000, 1280, 1280),
+    (16, 257, 136, 192)])
 def test_gemm_variants(eng, variant, M, N, K):
     rng = np.random.default_rng(M * 7 + N)
     A = rng.uniform(-1, 1, (M, K)).astype(np.float16)
@@ -40,9 +42,9 @@ def test_gemm_variants(eng, variant, M, N, K):
 @pytest.mark.parametrize("M,N,K", [(1500, 1280, 1280), (3000, 2304, 1280), (1500, 1280, 5120), (777, 264, 128)])
 def test_tile_sizes_bit_identical(eng, M, N, K):
     """The encoder GEMM picks its tile by M (64 for one or a few windows, with or without
-    the deep LDS ring, 128 with or without the 4-slot ring, or the
-    8-phase 256 at large M): every output element is the same MFMA chain over K in the
-    same order, so a window's encoder output does not depend on its batch."""
+    the deep LDS ring, 128 with or without the 4-slot ring, the half-width 256 x 128
+    8-wave tile, or the 8-phase 256 at large M): every output element is the same MFMA
+    chain over K in the same order, so a window's encoder output does not depend on its batch."""
     rng = np.random.default_rng(M + N + K)
     A = rng.uniform(-1, 1, (M, K)).astype(np.float16)
     W = rng.uniform(-1, 1, (N, K)).astype(np.float16)
@@ -51,7 +53,9 @@ def test_tile_sizes_bit_identical(eng, M, N, K):
     c7, _ = eng.debug_gemm(A, W, 7)
     c4, _ = eng.debug_gemm(A, W, 4)
     c11, _ = eng.debug_gemm(A, W, 11)
+    c16, _ = eng.debug_gemm(A, W, 16)
     assert np.array_equal(c1, c11)
+    assert np.array_equal(c1, c16)
     assert np.array_equal(c1, c6)
     assert np.array_equal(c1, c7)
     assert np.array_equal(c1, c4)
@@ -72,8 +76,11 @@ def test_8phase_transposed_epilogues_bit_identical(eng, M, N, K):
 
     c8, c12 = f16(eng.debug_gemm(A, W, 8)[0]), f16(eng.debug_gemm(A, W, 12)[0])
     c10, c13 = f16(eng.debug_gemm(A, W, 10)[0]), f16(eng.debug_gemm(A, W, 13)[0])
+    c18, c19 = f16(eng.debug_gemm(A, W, 18)[0]), f16(eng.debug_gemm(A, W, 19)[0])  # the half-width tile
     assert np.array_equal(c8, c12)
     assert np.array_equal(c10, c13)
+    assert np.array_equal(c8, c18)
+    assert np.array_equal(c10, c19)
     ref = A.astype(np.float64) @ W.astype(np.float64).T
     from scipy.special import erf
     gelu = 0.5 * ref * (1.0 + erf(ref / np.sqrt(2.0)))

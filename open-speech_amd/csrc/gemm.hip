@@ -1272,8 +1272,8 @@ int grid8(const GemmArgs& g) {
 // The half-width tile for few-window encoder GEMMs (profiles/r06_s2b_small_gemm.jsonl: every
 // tile variant on the five encoder shapes at 1-4 windows).  A half tile costs about half a
 // 256² tile, so with G workgroups the two grids take ceil(T/G) and ½·ceil(2T/G) tile rounds:
-// the half tile where that is fewer (one window: qkv, fc1 fill one round instead of a third
-// of the CUs; three and four windows: a 1.05-1.4-round 256² grid becomes 1.5 rounds' worth),
+// the half tile where that is fewer (three and four windows: a 1.05-1.4-round 256² grid
+// becomes 1.5 rounds' worth; the out-projection and fc2 at 3-4 windows fill one round),
 // from 90 256² tiles (below that the 64 / 128 tiles' 2-8x the workgroups win: the
 // out-projection and fc2 at one or two windows) up to 512 (the 64-window batches keep the
 // tuned 8-phase grid and its 32 KiB of LDS left for other lanes' decoders: the half tile's
@@ -1284,6 +1284,10 @@ bool use_half_tile(const GemmArgs& g, int64_t t8) {
         return !(e && e[0] == '0');
     }();
     if (!on || g.A_lo || g.kc != 0 || g.N % 8 != 0 || t8 < 90 || t8 >= 512) return false;
+    // below 180 256² tiles the alternative is the 64 / 128 family, whose fp16 epilogues
+    // measured as fast at one window in the whole encoder (5.86 vs 5.93 ms, r06_s2c): the
+    // half tile there only for the fp32 (residual) outputs, the out-projection and fc2
+    if (t8 < 180 && g.epi != EPI_F32_RESID && g.epi != EPI_F32) return false;
     const int64_t G = grid8(g), th = (int64_t)((g.N + 127) / 128) * ((g.M + GB - 1) / GB);
     return ((th + G - 1) / G) < 2 * ((t8 + G - 1) / G);
 }

@@ -26,13 +26,15 @@ for w in wins:
     win = [(i, 0, min(3000, nf[i] - 1)) for i in range(w)]
     for _ in range(3):
         eng.encode(win)
-    ts = []
+    ts, parts = [], []
     for _ in range(10):
         eng.set_profiling(True)  # resets the accumulated timers
         eng.encode(win)
         p = eng.profile()
         ts.append(p["encoder_ms"] + p["crosskv_ms"])
-    ts.sort()
-    out[f"w{w}_ms"] = round(ts[len(ts) // 2], 3)
+        parts.append((p["enc_gemm_ms"], p["enc_attn_ms"]))
+    i = sorted(range(len(ts)), key=ts.__getitem__)[len(ts) // 2]
+    out[f"w{w}_ms"] = round(ts[i], 3)
+    out[f"w{w}_gemm_attn_ms"] = [round(parts[i][0], 3), round(parts[i][1], 3)]
 print(json.dumps(out), flush=True)
 eng.close()

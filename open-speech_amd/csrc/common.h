@@ -169,7 +169,7 @@ int launch_gemm_skinny_partial(const GemmArgs& g, float* part, hipStream_t s);
 struct ProArgs;
 int launch_gemm_skinny_gelu_tail(const GemmArgs& g, float* part, const ProArgs& pa, hipStream_t s);
 int launch_gemm_skinny_pro(const GemmArgs& g, int pro, const ProArgs& pa, bool direct, float* part, hipStream_t s,
-                           bool select = false);
+                           bool select = false, bool attn_tail = false);
 void launch_layernorm(const float* x, int64_t M, int D, const float* g, const float* b, h16* y, hipStream_t s);
 
 }  // namespace osw

@@ -26,6 +26,8 @@ namespace osw {
 
 namespace {
 #include "select.h"
+constexpr int HD = 64;
+#include "selfattn.h"
 
 constexpr int BM = 128, BN = 128, BK = 64, NTHR = 256;
 #ifndef OSW_SKINNY_CK1
@@ -1926,6 +1928,28 @@ store:
                                         __HIP_MEMORY_SCOPE_AGENT);
             }
     }
+    if constexpr (TAIL == TAIL_ATTN) {
+        // batch-1 qkv projection (PRO_RESLN, split-K slabs): column block bx is q, k or v of
+        // head bx % H; the last of a head's 3 x ks workgroups to finish runs that head's
+        // self-attention (self_attn_one, the standalone kernel's function: same bits), so the
+        // self-attention is not launched.  Every slab store of this workgroup is complete at
+        // device scope before its ticket; the tail reads the slabs with device-scope loads.
+        static_assert(!DIRECT && PRO == PRO_RESLN && !SEL && MT == 1, "the attention tail serves the batch-1 qkv GEMM");
+        __shared__ int a_last;
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        const SelfAttnTail& at = pa.attn;
+        const int nks = g.K / kc, hh = bx % at.H;
+        if (threadIdx.x == 0) {
+            int* tk = pa.tail_ticket + hh;
+            a_last = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 3 * nks - 1;
+            if (a_last) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (!a_last) return;
+        self_attn_one<true, true>(part, nks, at.bias, at.kc, at.vc, at.pos, at.H, 1, at.ctx, at.out, at.lo_off, at.st,
+                                  at.pos_row, 0, hh);
+    }
     if constexpr (TAIL == TAIL_GELU) {
         static_assert(!DIRECT && PRO == PRO_NONE && !SEL, "the GELU tail reduces split-K slabs");
         // the last of the block's ks workgroups reduces its 64 columns x ROWS rows; every
@@ -2289,7 +2313,7 @@ int launch_gemm_skinny_gelu_tail(const GemmArgs& g0, float* part, const ProArgs&
 // the operand is built by the prologue (resln.h).  direct: one K range, EPI_F32 straight into g.C (the logits); otherwise the
 // split-K slabs into part, as launch_gemm_skinny_partial.  Returns ksplit.
 int launch_gemm_skinny_pro(const GemmArgs& g0, int pro, const ProArgs& pa, bool direct, float* part, hipStream_t s,
-                           bool select) {
+                           bool select, bool attn_tail) {
     GemmArgs g = g0;
     const int ks = direct ? 1 : skinny_ksplit(g.N, g.K);
     const dim3 grid((g.N + 63) / 64, ks, 1);
@@ -2302,6 +2326,12 @@ int launch_gemm_skinny_pro(const GemmArgs& g0, int pro, const ProArgs& pa, bool 
         if (!direct || pro != PRO_RESLN || g.M != 1 || g.epi != EPI_F32 || g.ldc != g.N)
             throw std::invalid_argument("fused selection: batch-1 logits GEMM only");
         gemm_skinny_kernel<1, true, EPI_F32, true, PRO_RESLN, true><<<grid, 256, 0, s>>>(g, kc, part, pa);
+        return ks;
+    }
+    if (attn_tail) {
+        if (direct || pro != PRO_RESLN || g.M != 1 || g.N != 3 * pa.attn.H * 64 || !pa.tail_ticket)
+            throw std::invalid_argument("attention tail: batch-1 qkv GEMM only");
+        gemm_skinny_kernel<1, false, EPI_F32, true, PRO_RESLN, false, TAIL_ATTN><<<grid, 256, 0, s>>>(g, kc, part, pa);
         return ks;
     }
     if (direct) {

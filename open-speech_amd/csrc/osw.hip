@@ -857,12 +857,33 @@ void decoder_step_fused(osw_ctx* c, int nb, int group, bool gather, const SelFus
         ks = launch_gemm_skinny_pro(gemm(nullptr, w, N, K), pro, pa, false, ps[last ^ 1], c->stream);
         last ^= 1;
     };
+    // OSW_B1_ATTN_TAIL=1: the self-attention as the qkv GEMM's last-arriver tail per head
+    // (TAIL_ATTN, the same device function as the standalone kernel, so the same bits; the
+    // whole GPU suite is green with it).  Measured slower: the tailed qkv takes 15.9 us per
+    // launch against 8.0 + 6.4 us for the GEMM and the self-attention kernel, batch-1 p50
+    // 111.4 / 111.6 vs 107.1 / 108.7 ms (profiles/r06_s2d_b1_attn_tail_ab.txt): the in-launch
+    // seam (ticket, device-scope slab loads) costs more than the kernel boundary it removes
+    static const bool attn_tail_on = [] {
+        const char* e = getenv("OSW_B1_ATTN_TAIL");
+        return e && e[0] == '1';
+    }();
+    const bool attn_tail = attn_tail_on && nb == 1 && !gather;
     for (int l = 0; l < L; ++l) {
         const std::string p = "dec.l" + std::to_string(l), pp = "dec.l" + std::to_string(l - 1);
-        fused(PRO_RESLN, l == 0 ? resln(nullptr, p + ".ln1", true) : resln(WF(c, pp + ".fc2.b"), p + ".ln1", false),
-              p + ".qkv.w", 3 * D, D);
-        launch_dec_self_attn(ps[last], ks, WF(c, p + ".qkv.b"), c->kc + l * kv_layer, c->vc + l * kv_layer, c->pos,
-                             nb, H, ctx, c->dattn, lo_d, gather ? c->anc : nullptr, group, c->sel, c->stream, c->row_pos);
+        ProArgs pq = l == 0 ? resln(nullptr, p + ".ln1", true) : resln(WF(c, pp + ".fc2.b"), p + ".ln1", false);
+        if (attn_tail) {
+            pq.tail_ticket = c->tail_ticket + 2048;  // [H] (the GELU tails use the first 160)
+            pq.attn = SelfAttnTail{WF(c, p + ".qkv.b"), c->kc + l * kv_layer, c->vc + l * kv_layer, c->pos, H, ctx,
+                                   c->row_pos ? 1 : 0, c->dattn, lo_d, c->sel};
+            ks = launch_gemm_skinny_pro(gemm(nullptr, p + ".qkv.w", 3 * D, D), PRO_RESLN, pq, false, ps[last ^ 1],
+                                        c->stream, false, true);
+            last ^= 1;
+        } else {
+            fused(PRO_RESLN, pq, p + ".qkv.w", 3 * D, D);
+            launch_dec_self_attn(ps[last], ks, WF(c, p + ".qkv.b"), c->kc + l * kv_layer, c->vc + l * kv_layer, c->pos,
+                                 nb, H, ctx, c->dattn, lo_d, gather ? c->anc : nullptr, group, c->sel, c->stream,
+                                 c->row_pos);
+        }
         plain(c->dattn, p + ".o.w", D, D);
         fused(PRO_RESLN, resln(WF(c, p + ".o.b"), p + ".ln2", false), p + ".xq.w", D, D);
         {

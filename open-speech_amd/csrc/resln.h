@@ -186,6 +186,18 @@ constexpr int PRO_ROWS = 1;      // rows the prologue serves: batch-1 latency (e
 constexpr int PRO_STRIDE = 1288; // halfs per LDS image row (D <= 1280; +8 staggers the banks)
 constexpr int GELU_ROWS = 8;     // PRO_GELU serves up to 8 rows: each workgroup reduces only its
 constexpr int GELU_KC = 256;     // own K range (<= GELU_KC deep), so no slab is read twice
+// TAIL_ATTN: the batch-1 self-attention run by the qkv GEMM's last arriver per head
+// (dec_self_attn_kernel's arguments; the slabs are the GEMM's own)
+struct SelfAttnTail {
+    const float* bias;   // qkv bias [3D]
+    h16* kc;             // this layer's self-K/V cache
+    h16* vc;
+    const int* pos;
+    int H, ctx, pos_row;
+    h16* out;            // attention output (hi; lo at out + lo_off)
+    int64_t lo_off;
+    const SelState* st;
+};
 struct ProArgs {
     ResLnArgs ln;        // PRO_RESLN: LayerNorm(x') of every row, all D columns
     const float* part;   // PRO_GELU: the fc1 slabs [ks][M][K], K = this GEMM's K
@@ -196,11 +208,12 @@ struct ProArgs {
     // row group) to finish reduces the block's slabs: y = gelu(bias + Σ_k part[k]) as a
     // hi/lo pair at tail_y[m * N + n] / tail_y[tail_lo + m * N + n], exactly as
     // dec_reduce_gelu_kernel (gelu_reduce_one's order), so that kernel is not launched.
-    int* tail_ticket;    // [column blocks x row groups], zero between launches
+    int* tail_ticket;    // [column blocks x row groups] (TAIL_ATTN: [heads]), zero between launches
     h16* tail_y;
     int64_t tail_lo;
+    SelfAttnTail attn;
 };
-enum Tail : int { TAIL_NONE = 0, TAIL_GELU = 1 };
+enum Tail : int { TAIL_NONE = 0, TAIL_GELU = 1, TAIL_ATTN = 2 };
 
 // fc1 -> fc2 operand: fp16 pair of gelu(bias + Σ_k part[k][r][n]), k in order (the order of
 // dec_reduce_gelu_kernel, which shares this function)

@@ -121,6 +121,24 @@ def test_turbo_batch64_equals_single_windows(turbo):
     assert k is None or float(z["margins"][k]) < NEAR_TIE, (k, float(z["margins"][k]))
 
 
+@pytest.mark.parametrize("n", [3, 4, 9])
+def test_turbo_encoder_few_windows_equal_single(turbo, n):
+    """The few-window encoders (streaming calls, session admissions) pick other GEMM tiles
+    than one window does — at 3-4 windows the half-width 256 x 128 tile for qkv (head-major
+    epilogue), fc1 (GELU) and the fp32 residual GEMMs, at 9 the 8-phase 256 tile (DESIGN
+    §5.12) — and every window's encoder output is bit-identical to the window encoded alone."""
+    d, eng, sup = turbo
+    clips = [synth.chirp_clip(40 + i, 30.0 - 2.5 * i) for i in range(n)]
+    nf = eng.log_mel(clips)
+    wins = [(i, 0, min(3000, nf[i] - 1)) for i in range(n)]
+    eng.encode(wins)
+    many = [eng.encoder_output(k) for k in range(n)]
+    for k in range(n):
+        eng.log_mel([clips[k]])
+        eng.encode([(0, 0, wins[k][2])])
+        assert np.array_equal(eng.encoder_output(0), many[k]), k
+
+
 def test_turbo_beam5_matches_fp32_golden(turbo):
     """Beam 5 on the benchmarked model: ids identical to the fp32 golden, cumulative
     log-prob within 1e-4 per token (+1e-3 relative), language and no-speech prob equal."""

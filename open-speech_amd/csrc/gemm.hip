@@ -1121,8 +1121,8 @@ void launch8p(const GemmArgs& g0, hipStream_t s) {
 // Two phases per K-tile — 1: quadrant (0,0) from A0 + W0, 2: quadrant (1,0) from A1 with
 // W0's fragments kept in registers — and a 3-slot ring of {A0, A1, W0} (144 KiB) so a
 // K-tile is staged two tiles ahead: phase 1 of tile t stages A0(t+2), W0(t+2) (their slots'
-// last reads were phase 1 of t-1, two phases back), phase 2 stages A1(t+2) and retires
-// tile t+1 (vmcnt(6): tile t+2's three half-tiles stay in flight).  Persistent like
+// last reads were phase 1 of t-1, two phases back), phase 2 stages A1(t+2); each half-tile
+// is waited for in the phase before its first read (three phases after its issue).  Persistent like
 // gemm8p_kernel (one workgroup per CU looping over tiles).
 constexpr int H8_SLOTS = 3, H8_LDS = H8_SLOTS * 3 * HT * 2;  // 147456 B
 static_assert(H8_LDS >= EPI_LDS, "the epilogue image fits the ring");
@@ -1199,35 +1199,44 @@ __device__ __forceinline__ void gemm8h_tile(const GemmArgs& g, int bid, h16* sme
     stage(0, 0);
     stage(2, 0);
     stage(1, 0);
+    // (each half-tile is retired by itself in the phase before the one that reads it: A0, W0
+    // of tile t+1 in phase 2 of tile t, A1 of tile t in phase 1 of tile t, so every half-tile
+    // has three phases from issue to wait)
     if (nk > 1) {
         stage(0, 1);
         stage(2, 1);
         stage(1, 1);
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A0, W0 of tile 0
     } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     }
     barrier();
     if (__builtin_amdgcn_readfirstlane(wave) >= 4) barrier();  // group 1 runs one barrier behind group 0
     for (int t = 0; t < nk; ++t) {
         const h16* buf = smem + (t % H8_SLOTS) * 3 * HT;
         const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
-        // phase 1: quadrant (0,0) from A0, W0
+        // phase 1: quadrant (0,0) from A0, W0; retire A1 of tile t
         if (n2) {
             stage(0, t + 2);
             stage(2, t + 2);
+            asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+        } else if (n1) {
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         read_a(buf + 0 * HT);
         read_b(buf + 2 * HT);
         barrier();
         mfma(0);
         barrier();
-        // phase 2: quadrant (1,0) from A1 (W0's fragments still in registers); retire tile t+1
+        // phase 2: quadrant (1,0) from A1 (W0's fragments still in registers); retire A0, W0
+        // of tile t+1
         if (n2) {
             stage(1, t + 2);
-            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         } else if (n1) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
         }
         read_a(buf + 1 * HT);
         barrier();

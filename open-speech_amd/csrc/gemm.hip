@@ -387,6 +387,9 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
     constexpr int NI = TN / 64;        // accumulator column blocks per wave
     constexpr int C16 = TN / 8;        // 16-B fp16 chunks per image row
     constexpr int C32 = TN / 4;        // 16-B fp32 chunks per image row
+    // (shifts and masks, not / and %: on the signed thread index those cost a sign fix-up each,
+    // which pushed the fp32-residual 8-phase epilogue from 250 VGPRs to 256 + 49 spilled)
+    constexpr int L16 = TN == 256 ? 5 : 4, L32 = TN == 256 ? 6 : 5;
     const int lane = tid & 63;
     // the bias of this thread's columns, loaded once per tile (epi_apply): TR, 4 columns per
     // accumulator block (one 16-B load each); otherwise one column per block
@@ -442,7 +445,7 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
 #pragma unroll 4
         for (int j = 0; j < 256 * C16 / GNT / NH; ++j) {
             const int id = j * GNT + tid;
-            const int row = half * 128 + id / C16, c8 = (id % C16) * 8;
+            const int row = half * 128 + (id >> L16), c8 = (id & (C16 - 1)) * 8;
             const int m = m0 + row, n = n0 + c8;
             if (m >= g.M || n >= g.N) continue;
             const h16x8 v = *(const h16x8*)&T[ep16(row, c8)];
@@ -462,7 +465,7 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
     } else {
         float* T = (float*)smem;
         // this thread's 4 copy-out columns are the same in every piece (GNT % 64 == 0)
-        const f32x4 b4 = hb ? *(const f32x4*)(g.bias + min(n0 + (tid % C32) * 4, g.N - 4))
+        const f32x4 b4 = hb ? *(const f32x4*)(g.bias + min(n0 + (tid & (C32 - 1)) * 4, g.N - 4))
                             : f32x4{-0.f, -0.f, -0.f, -0.f};
         for (int half = 0; half < 2; ++half) {
             if (IL || wm == half) {
@@ -491,7 +494,7 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
 #pragma unroll
             for (int jj = 0; jj < AB; ++jj) {
                 const int id = (j0 + jj) * GNT + tid;
-                const int row = id / C32, c4 = (id % C32) * 4;
+                const int row = id >> L32, c4 = (id & (C32 - 1)) * 4;
                 const int m = min(m0 + half * 128 + row, g.M - 1), n = min(n0 + c4, g.N - 4);
                 if constexpr (EPI == EPI_F32_RESID)
                     aux[jj] = *(const f32x4*)((float*)g.C + c_row(g, m) + n);
@@ -502,7 +505,7 @@ __device__ __forceinline__ void staged_epilogue(const GemmArgs& g, f32x4 (&acc)[
             for (int jj = 0; jj < AB; ++jj) {
                 const int j = j0 + jj;
                 const int id = j * GNT + tid;
-                const int row = id / C32, c4 = (id % C32) * 4;
+                const int row = id >> L32, c4 = (id & (C32 - 1)) * 4;
                 const int m = m0 + half * 128 + row, n = n0 + c4;
                 if (m < g.M && n < g.N) {
                     f32x4 v = *(const f32x4*)&T[ep32(row, c4)] + b4;

@@ -45,7 +45,7 @@ __device__ __forceinline__ void reduce_head(const float* __restrict__ part, int 
 // first K/V batch before the slab reduction left the batch-1 p50 unchanged, measured.)
 // GATHER (beam rows): the row's ancestry is loaded before the slab reduction and staged in
 // LDS behind its barrier, so it lands with the slabs (one round trip) instead of after.
-template <bool GATHER, bool VPRE>
+template <bool GATHER, bool VPRE, bool KALL = false>
 __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restrict__ part, int ks,
                                                             const float* __restrict__ bias, h16* __restrict__ kcache,
                                                             h16* __restrict__ vcache, const int* __restrict__ pos_ptr,
@@ -67,7 +67,8 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
         h = blockIdx.x % H;
         b = blockIdx.x / H;
         // (selfattn.h: the batch-1 qkv GEMM's TAIL_ATTN runs the same function)
-        self_attn_one<VPRE, false>(part, ks, bias, kcache, vcache, pos_ptr, H, B, ctx, out, lo_off, st, pos_row, b, h);
+        self_attn_one<VPRE, false, KALL>(part, ks, bias, kcache, vcache, pos_ptr, H, B, ctx, out, lo_off, st, pos_row,
+                                         b, h);
         return;
     }
     // every load of the prologue in one round trip: the row's state and position, its
@@ -1396,6 +1397,12 @@ void launch_dec_self_attn(const float* part, int ks, const float* bias, h16* kc,
         return e ? atoi(e) : 8;
     }();
     const bool vlate = vpre_env < 0 ? B > vpre_rows : vpre_env == 0;
+    // OSW_SELF_KALL (A/B switch; bit 1: the V-late form, bit 2: the VPRE form): both 256-key
+    // blocks' K (and V) pieces issued before any is used (attend_one KALL; same bits)
+    static const int kall = [] {
+        const char* e = std::getenv("OSW_SELF_KALL");
+        return e ? atoi(e) : 0;
+    }();
     if (anc) {  // ctx <= 448 (osw.hip checks the context at decode)
         if (vlate)
             dec_self_attn_kernel<true, false><<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, lo_off,
@@ -1404,11 +1411,19 @@ void launch_dec_self_attn(const float* part, int ks, const float* bias, h16* kc,
             dec_self_attn_kernel<true, true><<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, lo_off,
                                                                    anc, group, st, pos_row);
     } else if (vlate) {
-        dec_self_attn_kernel<false, false><<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, lo_off,
-                                                                 nullptr, 1, st, pos_row);
+        if (kall & 1)
+            dec_self_attn_kernel<false, false, true><<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out,
+                                                                           lo_off, nullptr, 1, st, pos_row);
+        else
+            dec_self_attn_kernel<false, false><<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, lo_off,
+                                                                     nullptr, 1, st, pos_row);
     } else {
-        dec_self_attn_kernel<false, true><<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, lo_off,
-                                                                nullptr, 1, st, pos_row);
+        if (kall & 2)
+            dec_self_attn_kernel<false, true, true><<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out,
+                                                                          lo_off, nullptr, 1, st, pos_row);
+        else
+            dec_self_attn_kernel<false, true><<<H * B, 256, 0, s>>>(part, ks, bias, kc, vc, pos, H, B, ctx, out, lo_off,
+                                                                    nullptr, 1, st, pos_row);
     }
 }
 

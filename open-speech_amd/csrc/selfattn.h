@@ -54,7 +54,10 @@ __device__ __forceinline__ h16x8 ld8(const h16* p) {
 // VPRE (the self-attention, MAXK = 448): each 256-key block's V pieces are issued with its K
 // pieces, so the P·V pass finds them landed (one HBM round trip per block instead of two);
 // the V pieces stay in registers across the softmax reductions.
-template <int MAXK, bool GATHER = false, bool NT = !GATHER, bool VPRE = false>
+// KALL (MAXK <= 512): both 256-key blocks' K pieces (and V pieces) are issued before any is
+// used, so a 448-key cache costs one round trip per pass instead of two; the FMAs run in the
+// same order, so the results are the same bits.
+template <int MAXK, bool GATHER = false, bool NT = !GATHER, bool VPRE = false, bool KALL = false>
 __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ K, const h16* __restrict__ V,
                            int n_keys, h16* __restrict__ out, int64_t lo_off, const int* soff = nullptr,
                            int64_t slot_stride = 0) {
@@ -80,6 +83,43 @@ __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ 
     for (int i = 0; i < 8; ++i) q[i] = qs[8 * c8 + i];
     float mx = -INFINITY;
     h16x8 vpre[VPRE ? NBLK : 1][8];
+    static_assert(!KALL || NBLK <= 2, "KALL holds at most two blocks of pieces");
+    auto kdots = [&](const h16x8 (&kv)[8], int base) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            float d = 0.f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) d = fmaf((float)kv[u][i], q[i], d);
+            d += xor_lane<1>(d);
+            d += xor_lane<2>(d);
+            d += xor_lane<4>(d);
+            const int key = base + u * 32 + kg;
+            if (key < n_keys) {
+                if (c8 == 0) sc[key] = d;
+                mx = fmaxf(mx, d);
+            }
+        }
+    };
+    if constexpr (KALL) {
+        h16x8 kv[NBLK][8];
+#pragma unroll
+        for (int blk = 0; blk < NBLK; ++blk) {
+            const int base = blk * 256;
+            if (base >= n_keys) break;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) kv[blk][u] = ld8<NT>(krow(K, min(base + u * 32 + kg, n_keys - 1)) + 8 * c8);
+            if constexpr (VPRE) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    vpre[blk][u] = ld8<NT>(krow(V, min(base + u * 32 + kg, n_keys - 1)) + 8 * c8);
+            }
+        }
+#pragma unroll
+        for (int blk = 0; blk < NBLK; ++blk) {
+            if (blk * 256 >= n_keys) break;
+            kdots(kv[blk], blk * 256);
+        }
+    } else {
     // 256 keys (8 loads per lane) per round trip: at most 2 for 448 keys
 #pragma unroll
     for (int blk = 0; blk < NBLK; ++blk) {
@@ -95,20 +135,8 @@ __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ 
 #pragma unroll
             for (int u = 0; u < 8; ++u) vpre[blk][u] = ld8<NT>(krow(V, min(base + u * 32 + kg, n_keys - 1)) + 8 * c8);
         }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            float d = 0.f;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) d = fmaf((float)kv[u][i], q[i], d);
-            d += xor_lane<1>(d);
-            d += xor_lane<2>(d);
-            d += xor_lane<4>(d);
-            const int key = base + u * 32 + kg;
-            if (key < n_keys) {
-                if (c8 == 0) sc[key] = d;
-                mx = fmaxf(mx, d);
-            }
-        }
+        kdots(kv, base);
+    }
     }
     mx = block_reduce_max(mx, red);
     float sum = 0.f;
@@ -121,6 +149,17 @@ __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ 
     // PV: thread -> (key group kg, d chunk c8), keys j = kg + 32 i; one wave-instruction
     // reads 8 consecutive V rows = 1 KiB contiguous
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // KALL without VPRE: every block's V pieces issued before the first block's FMAs
+    h16x8 vall[KALL && !VPRE ? NBLK : 1][8];
+    if constexpr (KALL && !VPRE) {
+#pragma unroll
+        for (int blk = 0; blk < NBLK; ++blk) {
+            const int j = kg + blk * 256;
+            if (blk * 256 >= n_keys) break;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) vall[blk][u] = ld8<NT>(krow(V, min(j + 32 * u, n_keys - 1)) + 8 * c8);
+        }
+    }
     // 8 V pieces per lane per round trip (keys past the end: clamped address, p = 0, so
     // the lane's keys are still accumulated in increasing order with nothing added)
 #pragma unroll
@@ -132,6 +171,7 @@ __device__ void attend_one(const h16* __restrict__ q16, const h16* __restrict__ 
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             if constexpr (VPRE) v[u] = vpre[blk][u];
+            else if constexpr (KALL) v[u] = vall[blk][u];
             else v[u] = ld8<NT>(krow(V, min(j + 32 * u, n_keys - 1)) + 8 * c8);
         }
 #pragma unroll
@@ -217,7 +257,7 @@ __device__ __forceinline__ void qkv_finish(const float* __restrict__ part, int k
 // projection's split-K slabs + bias, k and v appended to the cache at the row's position,
 // then attend over positions 0..pos.  A finished row reads and writes nothing more.
 // DEV: the slabs come from other workgroups of the calling launch (TAIL_ATTN).
-template <bool VPRE, bool DEV>
+template <bool VPRE, bool DEV, bool KALL = false>
 __device__ __forceinline__ void self_attn_one(const float* __restrict__ part, int ks, const float* __restrict__ bias,
                                               h16* __restrict__ kcache, h16* __restrict__ vcache,
                                               const int* __restrict__ pos_ptr, int H, int B, int ctx,
@@ -237,5 +277,5 @@ __device__ __forceinline__ void self_attn_one(const float* __restrict__ part, in
     qkv_finish<DEV>(part, ks, slab, row, D, h, L, q16, kc + (int64_t)pos * HD, vc + (int64_t)pos * HD);
     __threadfence_block();
     __syncthreads();
-    attend_one<448, false, true, VPRE>(q16, kc, vc, pos + 1, out + (int64_t)b * D + h * HD, lo_off);
+    attend_one<448, false, true, VPRE, KALL>(q16, kc, vc, pos + 1, out + (int64_t)b * D + h * HD, lo_off);
 }

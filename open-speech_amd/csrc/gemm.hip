@@ -1073,6 +1073,30 @@ __global__ __launch_bounds__(GNT, 1) void gemm8p_kernel(GemmArgs g) {
     }
 }
 
+// The persistent encoder GEMMs' grid (launch8p, launch8h): one workgroup per CU, or 3/4 of
+// the CUs (a multiple of the 8 XCDs) while sibling lanes have calls in flight, so the other
+// quarter never holds an encoder workgroup and another lane's decoder kernels run there at
+// full occupancy (256 CUs: 192 workgroups, 4768 -> 4872 audio-s/s; 224: 4864, 160: 4855,
+// measured).  OSW_GEMM_GRID=n: at most n workgroups while the CUs are shared;
+// OSW_GEMM_PERSIST=0: no cap (one workgroup per tile).
+int grid8(const GemmArgs& g) {
+    static const int cus = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return 256;
+        return n;
+    }();
+    static const bool per_tile = [] {
+        const char* e = std::getenv("OSW_GEMM_PERSIST");
+        return e && e[0] == '0';
+    }();
+    static const int shared_cap = [] {
+        if (const char* gg = std::getenv("OSW_GEMM_GRID")) return std::max(8, std::min(cus, atoi(gg)) / 8 * 8);
+        return std::max(8, cus * 3 / 4 / 8 * 8);
+    }();
+    return per_tile ? 1 << 30 : std::max(8, g.share_cus ? shared_cap : cus);
+}
+
 template <int EPI, int DBG = 0>
 void launch8p(const GemmArgs& g0, hipStream_t s) {
     constexpr int lds = EPI_LDS > 8 * HT * 2 ? EPI_LDS : 8 * HT * 2;
@@ -1092,27 +1116,7 @@ void launch8p(const GemmArgs& g0, hipStream_t s) {
     const bool next0 = next0_env < 0 ? EPI == EPI_F16_GELU : next0_env == 1;
     g.kc = next0 ? 1 : 0;  // (kc is unused by the 8-phase kernel otherwise)
     const int nwg = ((g.N + GB - 1) / GB) * ((g.M + GB - 1) / GB);
-    static const int cus = [] {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            return 1 << 30;
-        return n;
-    }();
-    static const bool per_tile = [] {  // OSW_GEMM_PERSIST=0: one workgroup per tile
-        const char* e = std::getenv("OSW_GEMM_PERSIST");
-        return e && e[0] == '0';
-    }();
-    static const int shared_cap = [] {
-        // OSW_GEMM_GRID=n: at most n workgroups while the CUs are shared
-        if (const char* gg = std::getenv("OSW_GEMM_GRID")) return std::max(8, std::min(cus, atoi(gg)) / 8 * 8);
-        // one workgroup per CU on 3/4 of the CUs (a multiple of the 8 XCDs): the other quarter
-        // never holds an encoder workgroup, so another lane's decoder kernels run there at full
-        // occupancy while this GEMM runs (256 CUs: 192 workgroups, 4768 -> 4872 audio-s/s;
-        // 224: 4864, 160: 4855, measured)
-        return std::max(8, cus * 3 / 4 / 8 * 8);
-    }();
-    const int grid_cap = per_tile ? 1 << 30 : g.share_cus ? shared_cap : cus;
-    gemm8p_kernel<EPI, DBG><<<std::min(nwg, std::max(8, grid_cap)), GNT, lds, s>>>(g);
+    gemm8p_kernel<EPI, DBG><<<std::min(nwg, grid8(g)), GNT, lds, s>>>(g);
 }
 
 // Half-width tile (256 x 128 x 64) for the encoder at one to a few windows, where the 256²
@@ -1269,18 +1273,6 @@ __global__ __launch_bounds__(GNT, 1) void gemm8h_kernel(GemmArgs g) {
         gemm8h_tile<EPI, DBG>(g, vb, smem, tid);
         __syncthreads();  // the epilogue's LDS image is the next tile's operand ring
     }
-}
-
-// The GEMM's persistent grid: every CU, or 3/4 of them while sibling lanes have calls in
-// flight (launch8p's rule)
-int grid8(const GemmArgs& g) {
-    static const int cus = [] {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            return 256;
-        return n;
-    }();
-    return g.share_cus ? std::max(8, cus * 3 / 4 / 8 * 8) : cus;
 }
 
 // The half-width tile for few-window encoder GEMMs (profiles/r06_s2b_small_gemm.jsonl: every

@@ -86,7 +86,7 @@ def parse(argv=None):
     ap.add_argument("--realistic-steps", type=int, default=9,
                     help="also time this many steps with realistic output lengths (random weights never emit "
                          "<|endoftext|>: each clip's length is forced from a seeded distribution)")
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r06_x_pmc.json"),
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r06_s2j_pmc.json"),
                     help="per-kernel HBM bytes from a rocprofv3 --pmc pass (tools/pmc_summary.py)")
     ap.add_argument("--standin", action="store_true",
                     help="launcher test only: ranks run a CPU stand-in engine over gloo (no GPU, no HIP library)")

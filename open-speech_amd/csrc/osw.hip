@@ -930,10 +930,16 @@ bool decoder_step(osw_ctx* c, int nb, int group, bool gather, const SelFuse* sf 
     auto partial = [&](const h16* A, int lda, const std::string& w, int N, int K) {
         const h16* Wt = WH(c, w);
         const int64_t lo = lda == 4 * D ? lo_4d : lo_d;
-        // > 64 rows, N > 1536: 128x128 split-K tiles; N <= 1536: skinny row groups (measured
-        // at 320 rows: N = 1280 11.4 vs 12.8 us, N = 3840 17.9 vs 12.8, N = 5120 21.7 vs 20.4)
-        static const int force = getenv("OSW_BEAM_GEMM") ? atoi(getenv("OSW_BEAM_GEMM")) : 0;  // 1 tiled, 2 skinny
-        if (nb > 64 && (force == 1 || (force == 0 && N > 1536))) {
+        // > 64 rows (beam search): skinny row groups for every projection.  Round 3 put N > 1536
+        // (qkv, fc1) on 64x128 split-K tiles (alone at 320 rows: N = 3840 12.8 vs 17.9 us,
+        // N = 5120 20.4 vs 21.7); round 6 re-measured the whole beam-5 bench on one box: 3-lane
+        // 3145 / 3138 (skinny everywhere) vs 3098 / 3104 audio-s/s (tiles for N > 1536), one
+        // lane 2617 / 2613 vs 2647 / 2650 (profiles/r06_s2k_beam_gemm_ab.txt): the 16-KiB skinny
+        // workgroups share the CUs with the other lanes' encoders better.  Same split-K depth
+        // (kc 256) and MFMA order either way: the same bits.  OSW_BEAM_GEMM=1: the tiles for
+        // N > 1536 (the round-3 choice), 3: tiles everywhere.
+        static const int force = getenv("OSW_BEAM_GEMM") ? atoi(getenv("OSW_BEAM_GEMM")) : 2;
+        if (nb > 64 && (force == 3 || (force == 1 && N > 1536))) {
             const int ks = tiled_ksplit(nb, N, K);
             REQUIRE((int64_t)ks * nb * N <= c->part_floats, "decoder workspace too small");
             GemmArgs g = gemm_plain(A, lda, Wt, nullptr, nb, N, K, nullptr, 0, EPI_F32);

@@ -2182,160 +2182,11 @@ void launch_wide256(const GemmArgs& g, int ks, hipStream_t s) {
     gemm_wide_kernel<LO, 256><<<dim3((g.N + 255) / 256, (g.M + WBM - 1) / WBM, ks), 512, lds, s>>>(g);
 }
 
-// Beam rows' vocabulary logits (65..320 hi/lo rows x N >= 16384, whole K): every row of
-// the batch in one workgroup, so the 133 MB weight matrix streams once from HBM straight into
-// VGPRs (fragment-major copy GemmArgs::Wf, one 1-KB fragment per wave-instruction) and the
-// activations (all MT*16 rows, hi and lo) are staged through LDS once per 64-deep K chunk and
-// shared by the 4 waves; the 64 x 256 tiles re-staged both operands per row tile (5 x the
-// weights at 320 rows, 974 MB of LDS-DMA per launch).  Wave = 32 columns (2 fragments), so
-// each activation fragment read from LDS feeds 2 x 2 MFMAs.  Transposed accumulators (Cᵀ =
-// W·Aᵀ, the 8-phase kernel's TR form: the same products in the same K order, hi then lo per
-// k32 step, as the skinny and wide kernels) so a lane holds 4 consecutive columns of one
-// row: 8-B stores.  Double-buffered A chunks: 2 x 2 x MT*16 x 64 halfs (160 KiB at MT = 20).
-template <int MT>
-__global__ __launch_bounds__(256, 1) void gemm_rows_kernel(GemmArgs g) {
-    extern __shared__ __attribute__((aligned(16))) h16 smem[];  // [2 bufs][hi, lo][MT*16][64]
-    constexpr int R = MT * 16, IMG = R * BK, AP = MT / 2;        // rows; halfs per image; glds per image
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, gq = lane >> 4;
-    const int n0 = blockIdx.x * 128 + wave * 32, m0 = blockIdx.y * R;  // grid y: row groups of R
-    const int nk = g.K / BK, ks32 = g.K >> 5;
-    const h16* wp[2];
-#pragma unroll
-    for (int f = 0; f < 2; ++f) {
-        const int blk = min(n0 + 16 * f, ((g.N + 15) & ~15) - 16) >> 4;
-        wp[f] = g.Wf + (int64_t)blk * ks32 * 512 + lane * 8;
-    }
-    // staging addresses recomputed per chunk (32-bit element offsets: 320 x 1280 rows): a
-    // 64-bit pointer per piece held across the loop cost 2 x MT VGPRs
-    const int r0 = wave * 8 + (lane >> 3), c0 = swz(r0, lane & 7) * 8;  // swz depends on row & 15: same for r0 + 32 i
-    const int64_t lo_off = g.A_lo - g.A;
-    auto stage = [&](int buf, int kt) {
-#pragma unroll
-        for (int im = 0; im < 2; ++im)
-#pragma unroll
-            for (int i = 0; i < AP; ++i) {
-                const int off = min(m0 + r0 + 32 * i, g.M - 1) * (int)g.lda + c0 + kt * BK;
-                __builtin_amdgcn_global_load_lds((const void*)(g.A + (im ? lo_off : 0) + off),
-                                                 (OSW_LDS void*)(smem + (buf * 2 + im) * IMG + (i * 4 + wave) * 8 * BK),
-                                                 16, 0, 0);
-            }
-    };
-    auto loadw = [&](h16x8 (&w)[2][2], int kt) {
-#pragma unroll
-        for (int st = 0; st < 2; ++st)
-#pragma unroll
-            for (int f = 0; f < 2; ++f) w[st][f] = *(const h16x8*)(wp[f] + (int64_t)(kt * 2 + st) * 512);
-    };
-    f32x4 acc[MT][2];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int f = 0; f < 2; ++f) acc[mt][f] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // one row tile's fragments read ahead of the current tile's MFMAs; the empty asm keeps
-    // the compiler from hoisting every tile's reads up front (MT x 4 fragments: spills)
-    auto compute = [&](int buf, const h16x8 (&w)[2][2]) {
-        const h16* hi = smem + (buf * 2) * IMG;
-        const h16* lo = hi + IMG;
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-            auto off = [&](int mt) {
-                const int row = mt * 16 + li;
-                return row * BK + swz(row, st * 4 + gq) * 8;
-            };
-            h16x8 ah = *(const h16x8*)&hi[off(0)], al = *(const h16x8*)&lo[off(0)];
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) {
-                h16x8 nh = ah, nl = al;
-                if (mt + 1 < MT) {
-                    nh = *(const h16x8*)&hi[off(mt + 1)];
-                    nl = *(const h16x8*)&lo[off(mt + 1)];
-                }
-#pragma unroll
-                for (int f = 0; f < 2; ++f) {
-                    acc[mt][f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w[st][f], ah, acc[mt][f], 0, 0, 0);
-                    acc[mt][f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w[st][f], al, acc[mt][f], 0, 0, 0);
-                }
-                asm volatile("" ::: "memory");
-                ah = nh;
-                al = nl;
-            }
-        }
-    };
-    h16x8 wa[2][2], wb[2][2];
-    loadw(wa, 0);
-    stage(0, 0);
-    for (int kt = 0; kt < nk; kt += 2) {
-        // chunk kt (buffer 0, weights wa); chunk kt+1's weights and activations in flight
-        if (kt + 1 < nk) {
-            loadw(wb, kt + 1);
-            stage(1, kt + 1);
-            wait_vmcnt<4 + 2 * AP>();
-        } else {
-            wait_vmcnt<0>();
-        }
-        __builtin_amdgcn_s_barrier();
-        compute(0, wa);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // buffer 0 free for chunk kt+2
-        if (kt + 1 >= nk) break;
-        if (kt + 2 < nk) {
-            loadw(wa, kt + 2);
-            stage(0, kt + 2);
-            wait_vmcnt<4 + 2 * AP>();
-        } else {
-            wait_vmcnt<0>();
-        }
-        __builtin_amdgcn_s_barrier();
-        compute(1, wb);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-    }
-    // lane: row mt*16 + li, columns n0 + 16 f + 4 gq .. +3 (8-B stores: the vocabulary row
-    // stride keeps rows 8-B aligned, not 16-B)
-    float* C = (float*)g.C;
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-        const int m = m0 + mt * 16 + li;
-        if (m >= g.M) continue;
-#pragma unroll
-        for (int f = 0; f < 2; ++f) {
-            const int n = n0 + 16 * f + 4 * gq;
-            float* dst = C + (int64_t)m * g.ldc + n;
-            if (n + 3 < g.N) {
-                *(float2*)dst = float2{acc[mt][f][0], acc[mt][f][1]};
-                *(float2*)(dst + 2) = float2{acc[mt][f][2], acc[mt][f][3]};
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if (n + e < g.N) dst[e] = acc[mt][f][e];
-            }
-        }
-    }
-}
-
-// the rows kernel for M hi/lo rows (65..320), or false (the caller keeps the wide kernel)
-bool launch_rows(const GemmArgs& g, hipStream_t s, bool force = false) {
-    static const bool on = [] {  // OSW_BEAM_LOGITS_ROWS=1 (A/B switch)
-        const char* e = std::getenv("OSW_BEAM_LOGITS_ROWS");
-        return e && e[0] == '1';
-    }();
-    if (!(on || force) || !g.A_lo || !g.Wf || g.M <= 64 || g.M > 320 || g.K % BK || g.kc != 0 || g.bias || g.ldc % 2)
-        return false;
-    // up to 192 rows in one row group; more (320 beam rows) in groups of 160 (MT = 10): all
-    // 320 rows in one workgroup (MT = 20) spilled 83 VGPRs
-    const int mt = (g.M + 15) / 16;
-    if (mt <= 8) gemm_rows_kernel<8><<<dim3((g.N + 127) / 128, 1), 256, 8 * 8192, s>>>(g);
-    else if (mt <= 12) gemm_rows_kernel<12><<<dim3((g.N + 127) / 128, 1), 256, 12 * 8192, s>>>(g);
-    else gemm_rows_kernel<10><<<dim3((g.N + 127) / 128, (g.M + 159) / 160), 256, 10 * 8192, s>>>(g);
-    return true;
-}
-
 void launch_wide(const GemmArgs& g, int ks, hipStream_t s) {
     // OSW_WIDE_N128=1 (A/B switch): the logits on the 64 x 128 tile too
     // OSW_WIDE256_ALL=1 (A/B switch): the split-K projections of beam rows on it as well
     static const bool n128 = getenv("OSW_WIDE_N128") != nullptr;
     static const bool all256 = getenv("OSW_WIDE256_ALL") != nullptr;
-    if (ks == 1 && g.N >= 16384 && launch_rows(g, s)) return;
     if (!n128 && ((ks == 1 && g.kc == 0 && g.N >= 16384) || all256)) {
         if (g.A_lo) launch_wide256<true>(g, ks, s);
         else launch_wide256<false>(g, ks, s);
@@ -2577,9 +2428,6 @@ void prepare_gemm_kernels() {
         set_lds_once((const void*)gemm8p_kernel<EPI_F16_GELU, 2>, l8p);
         set_lds_once((const void*)gemm_wide_kernel<true, 256>, wide_lds<256>(true));
         set_lds_once((const void*)gemm_wide_kernel<false, 256>, wide_lds<256>(false));
-        set_lds_once((const void*)gemm_rows_kernel<8>, 8 * 8192);
-        set_lds_once((const void*)gemm_rows_kernel<12>, 12 * 8192);
-        set_lds_once((const void*)gemm_rows_kernel<10>, 10 * 8192);
     });
 }
 
@@ -2639,10 +2487,6 @@ void launch_gemm_variant(const GemmArgs& g, int variant, hipStream_t s) {
     }
     if (variant == 15) {
         launch8p<EPI_F16, 3>(g, s);
-        return;
-    }
-    if (variant == 20) {  // debug: the beam-rows logits kernel (hi/lo A, fragment-major W)
-        if (!launch_rows(g, s, true)) throw std::invalid_argument("rows kernel: 65..320 hi/lo rows with Wf");
         return;
     }
     if (variant == 17) {  // debug: the half-width tile's main loop alone

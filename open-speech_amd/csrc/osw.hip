@@ -2419,7 +2419,6 @@ int osw_debug_gemm(osw_ctx* c, int32_t M, int32_t N, int32_t K, int32_t variant,
         REQUIRE(c && A && Wt && C && ms, "null argument");
         REQUIRE(M >= 1 && N >= 1 && K >= 64 && K % 64 == 0 && iters >= 1, "bad GEMM shape");
         REQUIRE(variant != 3 || (M <= 64 && K % 128 == 0), "skinny needs M <= 64 and K % 128 == 0");
-        REQUIRE(variant != 20 || (M > 64 && M <= 320 && N % 2 == 0), "the rows kernel takes 65..320 rows, even N");
         REQUIRE(variant < 8 || variant > 19 || variant == 11 || N % 8 == 0,
                 "the 8-phase debug variants need N % 8 == 0 (their epilogues store 8-column chunks)");
         std::lock_guard<std::mutex> lk(c->mu);
@@ -2430,12 +2429,6 @@ int osw_debug_gemm(osw_ctx* c, int32_t M, int32_t N, int32_t K, int32_t variant,
         h16* dW = dalloc<h16>((size_t)N * K, tmp);
         float* dC = dalloc<float>((size_t)M * N, tmp);
         float* dP = variant == 3 ? dalloc<float>((size_t)skinny_ksplit(N, K) * M * N, tmp) : nullptr;
-        // variants 5 / 20 with hi/lo activations (the decoder's form): A_lo = A - fp16(A) = 0
-        // for fp16 inputs, so the results stay those of the plain product; 20 reads the
-        // fragment-major copy of W
-        const bool hilo = variant == 20 || variant == 21;
-        h16* dAlo = hilo ? dalloc<h16>((size_t)M * K, tmp) : nullptr;
-        h16* dWf = hilo ? dalloc<h16>((size_t)((N + 15) / 16) * 16 * K, tmp) : nullptr;
         hipEvent_t e0, e1;
         HIPCHK(hipEventCreate(&e0));
         HIPCHK(hipEventCreate(&e1));
@@ -2443,15 +2436,8 @@ int osw_debug_gemm(osw_ctx* c, int32_t M, int32_t N, int32_t K, int32_t variant,
             HIPCHK(hipMemcpyAsync(dA, A, (size_t)M * K * 2, hipMemcpyHostToDevice, c->stream));
             HIPCHK(hipMemcpyAsync(dW, Wt, (size_t)N * K * 2, hipMemcpyHostToDevice, c->stream));
             GemmArgs g = gemm_plain(dA, K, dW, nullptr, M, N, K, dC, N, EPI_F32);
-            if (hilo) {
-                HIPCHK(hipMemsetAsync(dAlo, 0, (size_t)M * K * 2, c->stream));
-                launch_frag_pack(dW, K, N, K, dWf, c->stream);
-                g.A_lo = dAlo;
-                g.Wf = dWf;
-            }
             auto run = [&] {
                 if (variant == 3) launch_gemm_skinny(g, dP, c->stream);
-                else if (variant == 21) launch_gemm_variant(g, 5, c->stream);  // the wide kernel, hi/lo form
                 else launch_gemm_variant(g, variant, c->stream);
             };
             run();  // warm

@@ -61,21 +61,6 @@ def test_tile_sizes_bit_identical(eng, M, N, K):
     assert np.array_equal(c1, c4)
 
 
-@pytest.mark.parametrize("M,N,K", [(320, 51866, 1280), (100, 20000, 384), (190, 16390, 256), (161, 40000, 640)])
-def test_beam_rows_logits_kernel_bit_identical(eng, M, N, K):
-    """The beam-rows logits kernel (debug variant 20: 65..320 hi/lo rows, fragment-major W,
-    row groups of up to 192 / 160 rows) equals the wide 64 x 256 kernel on the same hi/lo
-    operands (variant 21) bit for bit, and the float64 product within fp32 accumulation."""
-    rng = np.random.default_rng(M + N + K)
-    A = rng.uniform(-1, 1, (M, K)).astype(np.float16)
-    W = rng.uniform(-1, 1, (N, K)).astype(np.float16)
-    c20, _ = eng.debug_gemm(A, W, 20)
-    c21, _ = eng.debug_gemm(A, W, 21)
-    assert np.array_equal(c20, c21)
-    ref = A.astype(np.float64) @ W.astype(np.float64).T
-    assert np.abs(c20 - ref).max() < 2e-3 * np.sqrt(K)
-
-
 @pytest.mark.parametrize("M,N,K", [(2048, 1280, 1280), (1000, 776, 192)])
 def test_8phase_transposed_epilogues_bit_identical(eng, M, N, K):
     """The 8-phase GEMM's fp16 epilogues run on transposed accumulators (Cᵀ = W·Aᵀ: the
